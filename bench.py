@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident CRC-32 throughput over ENet packet batches (BASELINE.json).
+
+    python bench.py [--gpus N --steps K --warmup W --config uniform|ragged|large]
+
+One step = one launch of the batch kernel over this rank's whole shard
+(default: 1M x 1200-byte packets = BASELINE configs[1]), inputs already resident
+in HBM.  N > 1 runs one process per GPU (torch.distributed.run); shards are
+independent (no data-path collective), so per-GPU work is fixed: weak scaling.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import rusty_enet_amd as rea  # noqa: E402
+from _data import ENET_SEED, packed_offsets, ragged_lengths  # noqa: E402
+
+METRIC = "device-resident GiB/s, batched CRC-32 over ENet packets; % HBM3E peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+CONFIGS = {
+    # name: (description, packets per GPU)
+    "uniform": ("1M x 1200-byte packets per GPU (ENet batch, uniform stride 1200)", 1 << 20),
+    "ragged": ("1M packets per GPU, lengths U{64..1392}, packed at byte offsets", 1 << 20),
+    "large": ("32768 x 64 KiB buffers per GPU (large-buffer path)", 32768),
+}
+
+
+def make_workload(name: str, rank: int, dev):
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED + 7919 * rank)
+    _, n = CONFIGS[name]
+    if name == "uniform":
+        L = 1200
+        data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        step = lambda: rea.crc32_batch(data, stride=L, length=L, count=n, out=out)  # noqa: E731
+        return step, n * L, n, out, ("uniform", data, L, L, n)
+    if name == "large":
+        L = 65536
+        data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        step = lambda: rea.crc32_batch(data, stride=L, length=L, count=n, out=out)  # noqa: E731
+        return step, n * L, n, out, ("uniform", data, L, L, n)
+    lengths = ragged_lengths(ENET_SEED + rank, n)
+    offsets = packed_offsets(lengths)
+    total = int(lengths.sum())
+    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    off = torch.from_numpy(offsets.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    step = lambda: rea.crc32_batch(data, offsets=off, lengths=ln, out=out)  # noqa: E731
+    return step, total, n, out, ("ragged", data, offsets, lengths)
+
+
+def verify_sample(out, spec, limit=20000) -> None:
+    """Bit-exact check of a sample of this rank's outputs against the oracle (not timed)."""
+    import _oracle
+
+    got = out.cpu().numpy().view(np.uint32)
+    if spec[0] == "uniform":
+        _, data, stride, length, n = spec
+        m = min(n, max(1, limit * 1200 // max(length, 1)))
+        host = data[: (m - 1) * stride + length].cpu().numpy()
+        want = _oracle.crc32_uniform(host, stride, length, m, threads=8)
+    else:
+        _, data, offsets, lengths = spec
+        m = min(len(lengths), limit)
+        end = int(offsets[m - 1]) + int(lengths[m - 1])
+        want = _oracle.crc32_ragged(data[:end].cpu().numpy(), offsets[:m], lengths[:m])
+    if not np.array_equal(got[:m], want):
+        raise SystemExit(f"bench: {int(np.count_nonzero(got[:m] != want))} of {m} checksums differ from the oracle")
+
+
+def cpu_baseline(seconds: float = 10.0) -> dict:
+    """src/crc32.rs restated in C (oracle/), timed on this host: BASELINE configs[0]."""
+    import _oracle
+    from _data import splitmix64_bytes
+
+    n, L = 4096, 1200
+    data = splitmix64_bytes(ENET_SEED, n * L)
+    _oracle.crc32_uniform(data, L, L, n)  # warm-up
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 20:
+        t0 = time.perf_counter()
+        _oracle.crc32_uniform(data, L, L, n)
+        times.append(time.perf_counter() - t0)
+    single = n * L / float(np.median(times)) / 2**30
+    threads = max(1, min(os.cpu_count() or 1, 16))
+    mt_times = []
+    big = np.tile(data, 8)  # 32768 packets so every thread has work
+    t_end = time.perf_counter() + seconds / 4
+    while time.perf_counter() < t_end or len(mt_times) < 10:
+        t0 = time.perf_counter()
+        _oracle.crc32_uniform(big, L, L, 8 * n, threads=threads)
+        mt_times.append(time.perf_counter() - t0)
+    multi = 8 * n * L / float(np.median(mt_times)) / 2**30
+    return {"value": round(single, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"4096 x 1200 B (BASELINE configs[0]), one crc32 call per packet, median of "
+                      f"{len(times)} passes over ~{seconds:.0f} s; C restatement of src/crc32.rs (no rustc here)",
+            "all_cores": {"value": round(multi, 4), "cores": threads}}
+
+
+def load_pmc_traffic(config: str):
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            v = json.load(f).get(config)
+        return None if v is None else v.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="uniform")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    step, nbytes, npk, out, spec = make_workload(args.config, rank, dev)
+    step()
+    torch.cuda.synchronize()
+    if not args.no_verify:
+        verify_sample(out, spec)
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)  # the stream crc32_batch launches on
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # average launch duration on that stream
+    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    wall_max, kernel_ms_max = float(t[0]), float(t[1])
+    ms_per_step = wall_max * 1000.0 / args.steps
+
+    if rank == 0:
+        total_bytes = nbytes * world
+        value = total_bytes / (ms_per_step / 1000.0) / 2**30
+        achieved = nbytes / (kernel_ms / 1000.0) / 1e9  # per-GPU algorithmic GB/s (rank 0)
+        traffic = load_pmc_traffic(args.config)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (torch.randint bytes on device, seeded)",
+            "config": {"workload": CONFIGS[args.config][0], "packets_per_gpu": npk, "bytes_per_gpu": nbytes,
+                       "parallelism": f"{world} independent shards, no collective"},
+            "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kernel_ms, 5), "kernel_ms_max_rank": round(kernel_ms_max, 5)},
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

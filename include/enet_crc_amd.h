@@ -1,0 +1,109 @@
+/*
+ * enet_crc_amd.h -- C ABI of the MI355X (gfx950) ENet CRC-32 checksum path.
+ *
+ * Drop-in for the checksum hook of jabuwu/rusty_enet v0.4.0:
+ *   - src/crc32.rs:39   pub fn crc32(in_buffers: &[&[u8]]) -> u32
+ *   - src/host.rs:40    HostSettings::checksum: Option<Box<dyn Fn(&[&[u8]]) -> u32>>
+ *   - src/c/protocol.rs:1470-1502 (receive verify) and :2255-2293 (send insert),
+ *     the two call sites of that hook.
+ *
+ * Every checksum this library returns equals the reference's value for the
+ * same bytes: bswap32(~reg) of the reflected-0xEDB88320 register started at
+ * 0xFFFFFFFF over the CONCATENATION of the input slices (src/crc32.rs:40-46).
+ *
+ * Conventions
+ *   - Plain C types only; the caller owns every buffer.
+ *   - Functions return an int status (ENET_CRC_OK = 0, negative on error).
+ *     Nothing here falls back to the CPU: without a usable HIP device the
+ *     calls fail with ENET_CRC_E_NO_DEVICE / ENET_CRC_E_HIP.
+ *   - "*_device" functions take device pointers and a hipStream_t passed as
+ *     void* (NULL = the legacy default stream); they are asynchronous and
+ *     run on the calling thread's current HIP device.
+ *   - A context (enet_crc_ctx) owns a stream plus pinned/device staging for
+ *     the host-memory entry points.  Calls on one context are serialised by
+ *     an internal lock, which is what lets the Rust adapter present it as the
+ *     `Fn` (not `FnMut`) closure HostSettings::checksum requires.
+ */
+#ifndef ENET_CRC_AMD_H
+#define ENET_CRC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ENET_CRC_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define ENET_CRC_API __attribute__((visibility("default")))
+#else
+#define ENET_CRC_API
+#endif
+
+#define ENET_CRC_OK 0
+#define ENET_CRC_E_INVALID (-1)   /* bad argument (NULL pointer, count overflow) */
+#define ENET_CRC_E_NO_DEVICE (-2) /* no HIP device / bad device index */
+#define ENET_CRC_E_HIP (-3)       /* a HIP runtime call failed; see enet_crc_last_hip_error() */
+#define ENET_CRC_E_NOMEM (-4)     /* host or device allocation failed */
+
+/* Shape of ENetBuffer {data, data_length} (src/c.rs:25-28): one input slice. */
+typedef struct enet_crc_iov {
+  const uint8_t* data;
+  size_t len;
+} enet_crc_iov;
+
+typedef struct enet_crc_ctx enet_crc_ctx;
+
+ENET_CRC_API int enet_crc_abi_version(void);
+ENET_CRC_API const char* enet_crc_strerror(int status);
+/* hipError_t of the last failing HIP call made by this thread (0 if none). */
+ENET_CRC_API int enet_crc_last_hip_error(void);
+/* Number of visible HIP devices (0 when none), or a negative status. */
+ENET_CRC_API int enet_crc_device_count(void);
+
+/* Create a context bound to HIP device `device` (its own non-blocking stream,
+ * pinned + device staging grown on demand). */
+ENET_CRC_API int enet_crc_ctx_create(int device, enet_crc_ctx** out_ctx);
+ENET_CRC_API void enet_crc_ctx_destroy(enet_crc_ctx* ctx);
+
+/*
+ * Per-call drop-in for `crc32(in_buffers)` (src/crc32.rs:39-47).
+ * Replaces: the closure stored in HostSettings::checksum (src/host.rs:40) and
+ * called at src/c/protocol.rs:1499 (one slice) and :2287 (up to 65 slices,
+ * BUFFER_MAXIMUM, src/consts.rs:37).  Slices may be empty or NULL-with-len-0.
+ * Gathers the slices into pinned staging, checksums on the GPU, writes the
+ * reference value to *out_crc.  Synchronous.
+ */
+ENET_CRC_API int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, uint32_t* out_crc);
+
+/*
+ * Device-resident uniform batch: packet p is the `length` bytes at
+ * d_base + p*stride, p in [0, count).  d_out[p] = crc32(&[packet p]).
+ * Replaces `count` calls of src/crc32.rs:39 with one launch.
+ */
+ENET_CRC_API int enet_crc32_uniform_device(const void* d_base, uint64_t stride, uint32_t length, uint64_t count,
+                              uint32_t* d_out, void* hip_stream);
+
+/*
+ * Device-resident ragged batch: packet p is d_lengths[p] bytes at
+ * d_base + d_offsets[p] (any byte alignment, packed or not).
+ */
+ENET_CRC_API int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                             uint64_t count, uint32_t* d_out, void* hip_stream);
+
+/*
+ * Host-resident ragged batch (the end-to-end path: host packet buffers such as
+ * the UdpSocket receive buffers of src/c/protocol.rs:1660-1680 in, checksums
+ * out).  Stages through pinned memory in chunks, overlapping copy and compute
+ * on the context's stream pair.  Synchronous.
+ */
+ENET_CRC_API int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t* h_offsets,
+                           const uint32_t* h_lengths, uint64_t count, uint32_t* h_out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* ENET_CRC_AMD_H */

@@ -1,0 +1,20 @@
+"""rusty_enet_amd: MI355X-native (gfx950 HIP) ENet per-datagram CRC-32.
+
+Drop-in for the checksum path of jabuwu/rusty_enet (src/crc32.rs and the
+HostSettings::checksum hook, src/host.rs:40).  See DESIGN.md / INTEGRATION.md.
+"""
+from ._native import CrcError, NativeLibraryMissing, LIB_PATH, HEADER_PATH  # noqa: F401
+from .checksum import (  # noqa: F401
+    Context,
+    checksum_fn,
+    crc32,
+    crc32_batch,
+    crc32_ragged_device,
+    crc32_uniform_device,
+    default_context,
+)
+
+__all__ = [
+    "Context", "CrcError", "NativeLibraryMissing", "checksum_fn", "crc32", "crc32_batch",
+    "crc32_ragged_device", "crc32_uniform_device", "default_context",
+]

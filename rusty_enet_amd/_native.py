@@ -1,0 +1,103 @@
+"""ctypes binding of the C ABI in include/enet_crc_amd.h.
+
+This is the Python equivalent of the cgo/JNI/Rust `extern "C"` stubs shown in
+INTEGRATION.md.  It only loads the in-tree shared library
+(rusty_enet_amd/lib/libenet_crc_amd.so, built by `make` / __graft_entry__.build()).
+If that file is missing the import of the compute functions raises: there is no
+Python or CPU fallback for the checksum.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libenet_crc_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                           "enet_crc_amd.h")
+
+ENET_CRC_OK = 0
+ENET_CRC_E_INVALID = -1
+ENET_CRC_E_NO_DEVICE = -2
+ENET_CRC_E_HIP = -3
+ENET_CRC_E_NOMEM = -4
+
+
+class NativeLibraryMissing(RuntimeError):
+    """The HIP extension was not built (run `make` or __graft_entry__.build())."""
+
+
+class CrcError(RuntimeError):
+    """A C-ABI call returned a negative status."""
+
+    def __init__(self, status: int, where: str, hip_error: int = 0):
+        self.status = status
+        self.hip_error = hip_error
+        msg = f"{where}: status {status}"
+        if _lib is not None:
+            msg += f" ({_lib.enet_crc_strerror(status).decode()})"
+        if hip_error:
+            msg += f", hipError {hip_error}"
+        super().__init__(msg)
+
+
+class Iov(ctypes.Structure):
+    """enet_crc_iov == ENetBuffer {data, data_length} (reference src/c.rs:25-28)."""
+
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+_SIGNATURES = {
+    "enet_crc_abi_version": (ctypes.c_int, []),
+    "enet_crc_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "enet_crc_last_hip_error": (ctypes.c_int, []),
+    "enet_crc_device_count": (ctypes.c_int, []),
+    "enet_crc_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "enet_crc_ctx_destroy": (None, [ctypes.c_void_p]),
+    "enet_crc32_iov": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Iov), ctypes.c_size_t, _u32p]),
+    "enet_crc32_uniform_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "enet_crc32_ragged_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "enet_crc32_ragged_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not found: build the HIP extension first (make, or "
+                "python -c 'import __graft_entry__ as g; g.build()')")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (restype, argtypes) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = restype
+            fn.argtypes = argtypes
+        if handle.enet_crc_abi_version() != 1:
+            raise NativeLibraryMissing("ABI version mismatch")
+        _lib = handle
+    return _lib
+
+
+def check(status: int, where: str) -> None:
+    if status != ENET_CRC_OK:
+        raise CrcError(status, where, lib().enet_crc_last_hip_error())
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGNATURES)

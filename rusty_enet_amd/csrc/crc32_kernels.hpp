@@ -1,0 +1,20 @@
+// Internal launcher interface between the C ABI (enet_crc_abi.hip) and the
+// gfx950 kernels (crc32_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace enet_crc {
+
+// Packets p = 0..count-1 at base + p*stride, each `length` bytes.
+hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
+                          uint32_t* out, hipStream_t stream);
+
+// Packets p at base + offsets[p], lengths[p] bytes (device arrays).
+hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+                         uint64_t count, uint32_t* out, hipStream_t stream);
+
+// Cached hipDeviceAttributeMultiprocessorCount of the calling thread's device.
+int cu_count_for_current_device();
+
+}  // namespace enet_crc

@@ -1,0 +1,325 @@
+// C ABI of the MI355X CRC-32 path (include/enet_crc_amd.h).
+//
+// The reference hook is a synchronous `Fn(&[&[u8]]) -> u32` called on the
+// thread running Host::service()/flush() (src/host.rs:185-201, src/c/protocol.rs
+// :1499 and :2287).  This file maps that surface and the batch entry points
+// onto the gfx950 kernels in crc32_kernels.hip.  There is no CPU path: every
+// checksum comes from the GPU or the call returns an error.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <new>
+
+#include "../../include/enet_crc_amd.h"
+#include "crc32_kernels.hpp"
+
+namespace enet_crc {
+
+namespace {
+
+thread_local int t_last_hip_error = 0;
+
+int fail_hip(hipError_t e) {
+  t_last_hip_error = (int)e;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return ENET_CRC_E_NO_DEVICE;
+  if (e == hipErrorOutOfMemory) return ENET_CRC_E_NOMEM;
+  return ENET_CRC_E_HIP;
+}
+
+#define ENET_HIP_TRY(expr)                 \
+  do {                                     \
+    hipError_t _e = (expr);                \
+    if (_e != hipSuccess) return fail_hip(_e); \
+  } while (0)
+
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cu_count[kMaxDevices];
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+int cu_count_for_current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
+  int n = g_cu_count[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+  g_cu_count[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+}  // namespace enet_crc
+
+using namespace enet_crc;
+
+// One pipeline slot of the host path: pinned input bytes + descriptors, device
+// copies, pinned output.
+struct StageSlot {
+  uint8_t* h_bytes = nullptr;
+  uint64_t* h_offsets = nullptr;
+  uint32_t* h_lengths = nullptr;
+  uint32_t* h_out = nullptr;
+  uint8_t* d_bytes = nullptr;
+  uint64_t* d_offsets = nullptr;
+  uint32_t* d_lengths = nullptr;
+  uint32_t* d_out = nullptr;
+  size_t byte_cap = 0;
+  size_t pkt_cap = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint64_t first = 0;  // packet range staged in this slot
+  uint64_t n = 0;
+  bool busy = false;
+};
+
+struct enet_crc_ctx {
+  int device = 0;
+  std::mutex lock;
+  StageSlot slot[2];
+};
+
+namespace {
+
+void free_slot_buffers(StageSlot& s) {
+  if (s.h_bytes) (void)hipHostFree(s.h_bytes);
+  if (s.h_offsets) (void)hipHostFree(s.h_offsets);
+  if (s.h_lengths) (void)hipHostFree(s.h_lengths);
+  if (s.h_out) (void)hipHostFree(s.h_out);
+  if (s.d_bytes) (void)hipFree(s.d_bytes);
+  if (s.d_offsets) (void)hipFree(s.d_offsets);
+  if (s.d_lengths) (void)hipFree(s.d_lengths);
+  if (s.d_out) (void)hipFree(s.d_out);
+  s.h_bytes = nullptr; s.h_offsets = nullptr; s.h_lengths = nullptr; s.h_out = nullptr;
+  s.d_bytes = nullptr; s.d_offsets = nullptr; s.d_lengths = nullptr; s.d_out = nullptr;
+  s.byte_cap = 0; s.pkt_cap = 0;
+}
+
+// Grows the slot to hold `bytes` input bytes and `pkts` packets (caller holds the ctx lock,
+// the slot is idle).
+int reserve_slot(StageSlot& s, size_t bytes, size_t pkts) {
+  bytes = std::max<size_t>(bytes, 4096);
+  pkts = std::max<size_t>(pkts, 64);
+  if (bytes > s.byte_cap) {
+    if (s.h_bytes) (void)hipHostFree(s.h_bytes);
+    if (s.d_bytes) (void)hipFree(s.d_bytes);
+    s.h_bytes = nullptr; s.d_bytes = nullptr; s.byte_cap = 0;
+    // +16: the kernel's 4-byte-grid loads never cross the packet's own words,
+    // but keep the staging allocation a whole number of 16-byte lines.
+    const size_t alloc = (bytes + 16 + 15) & ~(size_t)15;
+    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_bytes, alloc, hipHostMallocDefault));
+    ENET_HIP_TRY(hipMalloc((void**)&s.d_bytes, alloc));
+    s.byte_cap = bytes;
+  }
+  if (pkts > s.pkt_cap) {
+    if (s.h_offsets) (void)hipHostFree(s.h_offsets);
+    if (s.h_lengths) (void)hipHostFree(s.h_lengths);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.d_offsets) (void)hipFree(s.d_offsets);
+    if (s.d_lengths) (void)hipFree(s.d_lengths);
+    if (s.d_out) (void)hipFree(s.d_out);
+    s.h_offsets = nullptr; s.h_lengths = nullptr; s.h_out = nullptr;
+    s.d_offsets = nullptr; s.d_lengths = nullptr; s.d_out = nullptr; s.pkt_cap = 0;
+    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_offsets, pkts * sizeof(uint64_t), hipHostMallocDefault));
+    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_lengths, pkts * sizeof(uint32_t), hipHostMallocDefault));
+    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_out, pkts * sizeof(uint32_t), hipHostMallocDefault));
+    ENET_HIP_TRY(hipMalloc((void**)&s.d_offsets, pkts * sizeof(uint64_t)));
+    ENET_HIP_TRY(hipMalloc((void**)&s.d_lengths, pkts * sizeof(uint32_t)));
+    ENET_HIP_TRY(hipMalloc((void**)&s.d_out, pkts * sizeof(uint32_t)));
+    s.pkt_cap = pkts;
+  }
+  return ENET_CRC_OK;
+}
+
+// Host path chunking: at most this many staged bytes / packets per slot.
+constexpr size_t kStageBytes = 64u << 20;
+constexpr size_t kStagePackets = 1u << 18;
+
+}  // namespace
+
+extern "C" {
+
+int enet_crc_abi_version(void) { return ENET_CRC_ABI_VERSION; }
+
+const char* enet_crc_strerror(int status) {
+  switch (status) {
+    case ENET_CRC_OK: return "ok";
+    case ENET_CRC_E_INVALID: return "invalid argument";
+    case ENET_CRC_E_NO_DEVICE: return "no usable HIP device";
+    case ENET_CRC_E_HIP: return "HIP runtime error";
+    case ENET_CRC_E_NOMEM: return "out of memory";
+    default: return "unknown status";
+  }
+}
+
+int enet_crc_last_hip_error(void) { return t_last_hip_error; }
+
+int enet_crc_device_count(void) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e == hipErrorNoDevice) return 0;
+  if (e != hipSuccess) return fail_hip(e);
+  return n;
+}
+
+int enet_crc_ctx_create(int device, enet_crc_ctx** out_ctx) {
+  if (!out_ctx) return ENET_CRC_E_INVALID;
+  *out_ctx = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return e == hipSuccess ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
+  if (device < 0 || device >= n) return ENET_CRC_E_NO_DEVICE;
+  enet_crc_ctx* ctx = new (std::nothrow) enet_crc_ctx();
+  if (!ctx) return ENET_CRC_E_NOMEM;
+  ctx->device = device;
+  DeviceGuard g(device);
+  for (auto& s : ctx->slot) {
+    hipError_t se = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (se == hipSuccess) se = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (se != hipSuccess) {
+      enet_crc_ctx_destroy(ctx);
+      return fail_hip(se);
+    }
+  }
+  *out_ctx = ctx;
+  return ENET_CRC_OK;
+}
+
+void enet_crc_ctx_destroy(enet_crc_ctx* ctx) {
+  if (!ctx) return;
+  {
+    DeviceGuard g(ctx->device);
+    for (auto& s : ctx->slot) {
+      if (s.stream) (void)hipStreamSynchronize(s.stream);
+      free_slot_buffers(s);
+      if (s.done) (void)hipEventDestroy(s.done);
+      if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+  }
+  delete ctx;
+}
+
+int enet_crc32_uniform_device(const void* d_base, uint64_t stride, uint32_t length, uint64_t count,
+                              uint32_t* d_out, void* hip_stream) {
+  if (count == 0) return ENET_CRC_OK;
+  if (!d_out || (!d_base && length > 0)) return ENET_CRC_E_INVALID;
+  hipError_t e = launch_uniform(static_cast<const uint8_t*>(d_base), stride, length, count, d_out,
+                                static_cast<hipStream_t>(hip_stream));
+  return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+}
+
+int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                             uint64_t count, uint32_t* d_out, void* hip_stream) {
+  if (count == 0) return ENET_CRC_OK;
+  if (!d_base || !d_offsets || !d_lengths || !d_out) return ENET_CRC_E_INVALID;
+  hipError_t e = launch_ragged(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, d_out,
+                               static_cast<hipStream_t>(hip_stream));
+  return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+}
+
+int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, uint32_t* out_crc) {
+  if (!ctx || !out_crc || (nbufs > 0 && !bufs)) return ENET_CRC_E_INVALID;
+  size_t total = 0;
+  for (size_t i = 0; i < nbufs; ++i) {
+    if (bufs[i].len > 0 && !bufs[i].data) return ENET_CRC_E_INVALID;
+    total += bufs[i].len;
+  }
+  if (total > 0xFFFFFFFFull) return ENET_CRC_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  DeviceGuard g(ctx->device);
+  StageSlot& s = ctx->slot[0];
+  int st = reserve_slot(s, total, 1);
+  if (st != ENET_CRC_OK) return st;
+  size_t pos = 0;  // concatenation, src/crc32.rs:41-42
+  for (size_t i = 0; i < nbufs; ++i) {
+    if (bufs[i].len) memcpy(s.h_bytes + pos, bufs[i].data, bufs[i].len);
+    pos += bufs[i].len;
+  }
+  if (total) ENET_HIP_TRY(hipMemcpyAsync(s.d_bytes, s.h_bytes, total, hipMemcpyHostToDevice, s.stream));
+  ENET_HIP_TRY(launch_uniform(s.d_bytes, 0, (uint32_t)total, 1, s.d_out, s.stream));
+  ENET_HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+  ENET_HIP_TRY(hipStreamSynchronize(s.stream));
+  *out_crc = s.h_out[0];
+  return ENET_CRC_OK;
+}
+
+int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t* h_offsets,
+                           const uint32_t* h_lengths, uint64_t count, uint32_t* h_out) {
+  if (!ctx) return ENET_CRC_E_INVALID;
+  if (count == 0) return ENET_CRC_OK;
+  if (!h_base || !h_offsets || !h_lengths || !h_out) return ENET_CRC_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  DeviceGuard g(ctx->device);
+  const uint8_t* base = static_cast<const uint8_t*>(h_base);
+
+  // Drain a slot: wait for its kernel + D2H, copy checksums out.
+  auto drain = [&](StageSlot& s) -> int {
+    if (!s.busy) return ENET_CRC_OK;
+    ENET_HIP_TRY(hipEventSynchronize(s.done));
+    memcpy(h_out + s.first, s.h_out, s.n * sizeof(uint32_t));
+    s.busy = false;
+    return ENET_CRC_OK;
+  };
+
+  uint64_t p = 0;
+  int which = 0;
+  while (p < count) {
+    StageSlot& s = ctx->slot[which];
+    int st = drain(s);
+    if (st != ENET_CRC_OK) return st;
+    // Chunk [p, q): packets whose byte span [lo, hi) fits the staging size.
+    uint64_t lo = h_offsets[p], hi = h_offsets[p] + h_lengths[p];
+    uint64_t q = p + 1;
+    while (q < count && q - p < kStagePackets) {
+      const uint64_t nlo = std::min<uint64_t>(lo, h_offsets[q]);
+      const uint64_t nhi = std::max<uint64_t>(hi, h_offsets[q] + h_lengths[q]);
+      if (nhi - nlo > kStageBytes) break;
+      lo = nlo; hi = nhi; ++q;
+    }
+    // Keep the device copy at the same offset mod 4 as the host bytes, so the
+    // kernel sees the same word grid (not required for correctness).
+    const uint64_t lo_al = lo & ~(uint64_t)3;
+    const size_t span = (size_t)(hi - lo_al);
+    st = reserve_slot(s, span, (size_t)(q - p));
+    if (st != ENET_CRC_OK) return st;
+    memcpy(s.h_bytes, base + lo_al, span);
+    for (uint64_t i = p; i < q; ++i) {
+      s.h_offsets[i - p] = h_offsets[i] - lo_al;
+      s.h_lengths[i - p] = h_lengths[i];
+    }
+    const size_t n = (size_t)(q - p);
+    ENET_HIP_TRY(hipMemcpyAsync(s.d_bytes, s.h_bytes, span, hipMemcpyHostToDevice, s.stream));
+    ENET_HIP_TRY(hipMemcpyAsync(s.d_offsets, s.h_offsets, n * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream));
+    ENET_HIP_TRY(hipMemcpyAsync(s.d_lengths, s.h_lengths, n * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
+    ENET_HIP_TRY(launch_ragged(s.d_bytes, s.d_offsets, s.d_lengths, n, s.d_out, s.stream));
+    ENET_HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+    ENET_HIP_TRY(hipEventRecord(s.done, s.stream));
+    s.first = p;
+    s.n = n;
+    s.busy = true;
+    p = q;
+    which ^= 1;
+  }
+  for (auto& s : ctx->slot) {
+    int st = drain(s);
+    if (st != ENET_CRC_OK) return st;
+  }
+  return ENET_CRC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// Host-side model of the gfx950 kernel's arithmetic (crc32_kernels.hip), lane by
+// lane, checked against the oracle restatement of src/crc32.rs.  Test
+// infrastructure only: it exercises the GF(2) operator tables
+// (rusty_enet_amd/csrc/crc32_ops.hpp), the end-aligned stream decomposition, the
+// head masking / init injection and the fixed-shift combine tree for every lane
+// count the kernel template allows, without a GPU.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../../rusty_enet_amd/csrc/crc32_ops.hpp"
+
+extern "C" {
+struct oracle_iov { const uint8_t* data; size_t len; };
+uint32_t oracle_crc32(const uint8_t* p, size_t n);
+const uint32_t* oracle_crc_table(void);
+}
+
+using namespace enet_crc;
+static const OpTables& T = kOpTables;
+
+static uint32_t op(int lv, uint32_t x) { return apply_op(T.op[lv], x); }
+
+template <int G>
+static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
+  const uint64_t sa = s, ea = s + len, top = sa & ~3ull, a1 = ea & ~3ull;
+  const uint64_t nwords = (a1 - top) >> 2;
+  constexpr int kMain = __builtin_ctz(4 * G);
+  uint32_t reg = kInitRegister;
+  if (nwords > 0) {
+    const uint64_t nchunks = (nwords + 3) >> 2;
+    const int64_t nsteps = (int64_t)((nchunks + G - 1) / G);
+    uint32_t h[G][4];
+    for (int k = 0; k < G; ++k) {
+      const int64_t c = k + (int64_t)G * (nsteps - 1);
+      for (int j = 0; j < 4; ++j) {
+        const int64_t rel = (int64_t)(a1 - top) - 16 * (c + 1) + 4 * j;
+        uint32_t w = 0;
+        if (rel >= 0) memcpy(&w, buf + top + rel, 4);
+        if (rel == 0) {
+          const uint32_t v = (uint32_t)(sa - top);
+          w = (w & (0xFFFFFFFFu << (8 * v))) ^ T.head_k[v];
+        }
+        h[k][j] = w;
+      }
+      for (int64_t i = nsteps - 2; i >= 0; --i) {
+        uint32_t q[4];
+        memcpy(q, buf + a1 - 16 * (k + G * i + 1), 16);
+        for (int j = 0; j < 4; ++j) h[k][j] = op(kMain, h[k][j]) ^ q[j];
+      }
+    }
+    uint32_t y[G];
+    for (int k = 0; k < G; ++k) y[k] = op(0, op(0, op(0, h[k][0]) ^ h[k][1]) ^ h[k][2]) ^ h[k][3];
+    for (int l = 1; (1 << l) <= G; ++l) {
+      const int d = 1 << (l - 1);
+      uint32_t t[G];
+      for (int k = 0; k < G; ++k) t[k] = op(l + 1, y[k]);
+      for (int k = 0; k + d < G; ++k) y[k] ^= t[k + d];
+    }
+    reg = op(0, y[0]);
+  }
+  for (uint64_t b = (a1 > sa ? a1 : sa); b < ea; ++b) reg = (reg >> 8) ^ T.sarwate[(reg ^ buf[b]) & 0xffu];
+  return __builtin_bswap32(~reg);
+}
+
+int main() {
+  int bad = 0;
+  const uint32_t* ot = oracle_crc_table();
+  for (int b = 0; b < 256; ++b) bad += T.sarwate[b] != ot[b];
+  for (int b = 0; b < 256; ++b) bad += T.op[0][3][b] != ot[b];  // M32(b<<24) == T[b]
+  // head_k[v] = M8^{-v}(~0): M8^v(head_k[v]) must give back ~0.
+  for (int v = 0; v < 4; ++v) {
+    uint32_t r = T.head_k[v];
+    for (int i = 0; i < v; ++i) r = (r >> 8) ^ T.sarwate[r & 0xff];
+    bad += r != 0xFFFFFFFFu;
+  }
+  if (bad) { printf("table mismatch %d\n", bad); return 1; }
+  std::mt19937_64 g(12345);
+  std::vector<uint8_t> buf(1 << 19);
+  for (auto& x : buf) x = (uint8_t)g();
+  long cases = 0;
+  for (int it = 0; it < 60000; ++it) {
+    const uint64_t s = g() % 4096;
+    const uint64_t len = it < 6000 ? (uint64_t)(it % 600) : g() % (it % 11 == 0 ? 300000 : 3000);
+    if (s + len > buf.size()) continue;
+    const uint32_t want = oracle_crc32(buf.data() + s, len);
+    const uint32_t got[4] = {model<2>(buf.data(), s, len), model<4>(buf.data(), s, len),
+                             model<8>(buf.data(), s, len), model<16>(buf.data(), s, len)};
+    for (uint32_t v : got) {
+      if (v != want) {
+        if (bad < 10) printf("mismatch s=%llu len=%llu want %08x got %08x\n", (unsigned long long)s,
+                             (unsigned long long)len, want, v);
+        ++bad;
+      }
+    }
+    ++cases;
+  }
+  printf("cases=%ld bad=%d\n", cases, bad);
+  return bad ? 1 : 0;
+}

@@ -1,0 +1,56 @@
+"""The C-ABI library loads, exports every symbol include/enet_crc_amd.h declares,
+and fails loudly (negative status, no CPU fallback) when no HIP device exists.
+No compute calls are made here."""
+import ctypes
+import re
+
+import pytest
+
+from rusty_enet_amd import _native
+
+
+def _declared_symbols():
+    with open(_native.HEADER_PATH) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"ENET_CRC_API\s+[\w\s\*]+?\b(enet_crc\w*)\s*\(", text)))
+
+
+def test_header_declares_expected_api():
+    syms = _declared_symbols()
+    assert "enet_crc32_iov" in syms and "enet_crc32_uniform_device" in syms
+    assert "enet_crc32_ragged_device" in syms and "enet_crc32_ragged_host" in syms
+    assert sorted(_native.exported_symbols()) == syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.lib()
+    for name in _declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.enet_crc_abi_version() == 1
+    assert lib.enet_crc_strerror(0) == b"ok"
+    assert lib.enet_crc_strerror(_native.ENET_CRC_E_NO_DEVICE) == b"no usable HIP device"
+
+
+def test_only_abi_symbols_are_exported():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    names = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    ours = {n for n in names if n.startswith("enet_")}
+    assert ours == set(_declared_symbols())
+
+
+def test_no_device_fails_loudly():
+    lib = _native.lib()
+    n = lib.enet_crc_device_count()
+    if n > 0:
+        pytest.skip("a HIP device is visible; the no-device path is exercised on CPU-only hosts")
+    handle = ctypes.c_void_p()
+    st = lib.enet_crc_ctx_create(0, ctypes.byref(handle))
+    assert st == _native.ENET_CRC_E_NO_DEVICE
+    assert not handle.value
+    import rusty_enet_amd
+    with pytest.raises(rusty_enet_amd.CrcError):
+        rusty_enet_amd.crc32([b"123456789"])
+    # device entry points validate arguments before touching the device
+    assert lib.enet_crc32_uniform_device(None, 0, 0, 0, None, None) == 0  # empty batch is a no-op
+    assert lib.enet_crc32_ragged_device(None, None, None, 5, None, None) == _native.ENET_CRC_E_INVALID

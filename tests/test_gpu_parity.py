@@ -1,0 +1,208 @@
+"""GPU parity: every checksum from the gfx950 kernels (through the C ABI) is
+bit-exact against the oracle restatement of src/crc32.rs and the zlib golden
+fixtures.  Run on an MI355X with  python -m pytest tests -m gpu.
+"""
+import numpy as np
+import pytest
+
+import _oracle
+from _data import ENET_SEED, packed_offsets, ragged_lengths, splitmix64_bytes
+
+torch = pytest.importorskip("torch")
+import rusty_enet_amd as rea  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def as_u32(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint32)
+
+
+def to_dev(a: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def ragged_on_device(data, offsets, lengths, dev):
+    d = to_dev(data, dev)
+    off = to_dev(offsets.astype(np.int64), dev)
+    ln = to_dev(lengths.astype(np.int32), dev)
+    out = rea.crc32_batch(d, offsets=off, lengths=ln)
+    torch.cuda.synchronize()
+    return as_u32(out)
+
+
+# --- the reference's own tests, through the per-call drop-in (enet_crc32_iov) ----
+
+def test_reference_kats_per_call(dev):
+    assert rea.crc32([bytes([1, 2, 3, 4, 5, 6, 7, 8])]) == 3314076223          # src/crc32.rs:52
+    assert rea.crc32([bytes([1, 2, 3, 4, 5, 6, 7, 8]),
+                      bytes([8, 7, 6, 5, 4, 3, 2, 1])]) == 1712484799          # src/crc32.rs:54-55
+
+
+def test_golden_kats_per_call(dev, golden):
+    ctx = rea.default_context(0)
+    for k in golden["kat"]:
+        assert ctx([bytes(s) for s in k["slices_bytes"]]) == k["expected"], k["name"]
+
+
+def test_golden_cases_per_call(dev, golden):
+    ctx = rea.default_context(0)
+    for case in golden["cases"]:
+        slices = [splitmix64_bytes(s, n) for s, n in case["slices"]]
+        assert ctx(slices) == case["expected"], case["name"]
+
+
+def test_golden_cases_in_one_ragged_batch(dev, golden):
+    # Every golden input concatenated, placed at deliberately misaligned offsets.
+    blobs = [b"".join(bytes(splitmix64_bytes(s, n)) for s, n in c["slices"]) for c in golden["cases"]]
+    offsets, pos, parts = [], 3, [b"\xAA" * 3]
+    for i, b in enumerate(blobs):
+        offsets.append(pos)
+        parts.append(b)
+        gap = i % 5
+        parts.append(b"\x55" * gap)
+        pos += len(b) + gap
+    data = np.frombuffer(b"".join(parts) + b"\x00" * 16, dtype=np.uint8)
+    got = ragged_on_device(data, np.array(offsets, dtype=np.uint64),
+                           np.array([len(b) for b in blobs], dtype=np.uint32), dev)
+    want = np.array([c["expected"] for c in golden["cases"]], dtype=np.uint32)
+    assert np.array_equal(got, want)
+
+
+# --- exhaustive small shapes ------------------------------------------------------
+
+def test_every_length_every_alignment(dev):
+    # lengths 0..700 at start offsets 0..15 (both the 4-byte grid and the 16-byte
+    # chunking see every phase), packed back to back.
+    lens, offs, pos = [], [], 0
+    for n in range(0, 701):
+        for a in range(16):
+            pos += a  # gap -> start phase varies
+            offs.append(pos)
+            lens.append(n)
+            pos += n
+    data = splitmix64_bytes(11, pos + 64)
+    offsets = np.array(offs, dtype=np.uint64)
+    lengths = np.array(lens, dtype=np.uint32)
+    got = ragged_on_device(data, offsets, lengths, dev)
+    assert np.array_equal(got, _oracle.crc32_ragged(data, offsets, lengths))
+
+
+def test_uniform_batch_1200(dev):
+    n, L = 65536, 1200
+    data = splitmix64_bytes(ENET_SEED, n * L)
+    d = to_dev(data, dev)
+    got = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
+    assert np.array_equal(got, _oracle.crc32_uniform(data, L, L, n, threads=8))
+
+
+@pytest.mark.parametrize("stride,length", [(1201, 1200), (1392, 1392), (1396, 1393), (64, 64), (7, 5), (4096, 4096)])
+def test_uniform_batch_shapes(dev, stride, length):
+    n = 20000
+    data = splitmix64_bytes(stride * 31 + length, (n - 1) * stride + length)
+    d = to_dev(data, dev)
+    got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
+    assert np.array_equal(got, _oracle.crc32_uniform(data, stride, length, n, threads=8))
+
+
+def test_large_buffers_64k(dev):
+    n, L = 256, 65536
+    data = splitmix64_bytes(77, n * L)
+    d = to_dev(data, dev)
+    got = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
+    assert np.array_equal(got, _oracle.crc32_uniform(data, L, L, n, threads=8))
+
+
+def test_large_unaligned_odd_lengths(dev):
+    lengths = np.array([65536 + 3, 100000, 1, 0, 262147, 4095, 70001], dtype=np.uint32)
+    offsets = packed_offsets(lengths) + np.uint64(1)
+    data = splitmix64_bytes(78, int(lengths.sum()) + 8)
+    got = ragged_on_device(data, offsets, lengths, dev)
+    assert np.array_equal(got, _oracle.crc32_ragged(data, offsets, lengths))
+
+
+# --- BASELINE.json full-size configs ------------------------------------------------
+
+def test_full_size_uniform_1m_x_1200(dev):
+    n, L = 1 << 20, 1200
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    got = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
+    want = _oracle.crc32_uniform(d.cpu().numpy(), L, L, n, threads=16)
+    assert np.array_equal(got, want)
+
+
+def test_full_size_ragged_1m(dev):
+    lengths = ragged_lengths(ENET_SEED, 1 << 20)
+    offsets = packed_offsets(lengths)
+    total = int(lengths.sum())
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED + 1)
+    d = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    out = rea.crc32_batch(d, offsets=to_dev(offsets.astype(np.int64), dev),
+                          lengths=to_dev(lengths.astype(np.int32), dev))
+    got = as_u32(out)
+    assert np.array_equal(got, _oracle.crc32_ragged(d.cpu().numpy(), offsets, lengths))
+
+
+# --- properties --------------------------------------------------------------------
+
+def test_single_bit_flips_are_detected(dev):
+    # The CRC is the corruption detector of src/c/protocol.rs:1499-1501: every
+    # single-bit error in a datagram must change its checksum.
+    n, L = 4096, 1200
+    data = splitmix64_bytes(5, n * L)
+    d = to_dev(data, dev)
+    base = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
+    rng = np.random.default_rng(0)
+    pos = np.arange(n) * L + rng.integers(0, L, n)
+    bits = rng.integers(0, 8, n)
+    flipped = data.copy()
+    flipped[pos] ^= (1 << bits).astype(np.uint8)
+    got = as_u32(rea.crc32_batch(to_dev(flipped, dev), stride=L, length=L, count=n))
+    assert np.all(got != base)
+    assert np.array_equal(got, _oracle.crc32_uniform(flipped, L, L, n, threads=8))
+
+
+def test_repeatable_and_stream_ordered(dev):
+    n, L = 50000, 1200
+    data = to_dev(splitmix64_bytes(6, n * L), dev)
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        a = rea.crc32_batch(data, stride=L, length=L, count=n, stream=s)
+        b = rea.crc32_batch(data, stride=L, length=L, count=n, stream=s)
+    s.synchronize()
+    assert torch.equal(a, b)
+
+
+def test_empty_batch_and_zero_length(dev):
+    d = torch.zeros(16, dtype=torch.uint8, device=dev)
+    out = rea.crc32_batch(d, stride=0, length=0, count=5)
+    assert np.array_equal(as_u32(out), np.zeros(5, dtype=np.uint32))  # crc32(&[]) == 0
+    out = rea.crc32_batch(d, stride=16, length=16, count=0)
+    assert out.numel() == 0
+
+
+def test_host_batch_end_to_end(dev):
+    lengths = ragged_lengths(9, 300000)
+    offsets = packed_offsets(lengths) + np.uint64(2)
+    data = splitmix64_bytes(10, int(lengths.sum()) + 8)
+    ctx = rea.Context(0)
+    got = ctx.crc32_ragged_host(data, offsets, lengths)
+    ctx.close()
+    assert np.array_equal(got, _oracle.crc32_ragged(data, offsets, lengths))
+
+
+def test_per_call_65_slices(dev):
+    # The send path passes a 65-slice array (BUFFER_MAXIMUM), most of them empty.
+    rng = np.random.default_rng(3)
+    for trial in range(20):
+        slices = [splitmix64_bytes(100 * trial + j, int(rng.integers(0, 40)) if j < 9 else 0) for j in range(65)]
+        assert rea.crc32(slices) == _oracle.crc32(slices)
