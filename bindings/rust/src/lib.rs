@@ -1,0 +1,127 @@
+//! Rust side of the drop-in: binds `include/enet_crc_amd.h` and produces the
+//! closure `rusty_enet::HostSettings::checksum` expects
+//! (`Option<Box<dyn Fn(&[&[u8]]) -> u32>>`, rusty_enet src/host.rs:40).
+//!
+//! ```ignore
+//! let gpu = enet_crc_amd::GpuCrc32::new(0)?;
+//! let settings = rusty_enet::HostSettings {
+//!     checksum: Some(gpu.checksum_fn()),   // was: Some(Box::new(rusty_enet::crc32))
+//!     ..Default::default()
+//! };
+//! ```
+//!
+//! Written against the C ABI only; this image has no Rust toolchain, so the
+//! crate is compiled where `cargo` exists.
+#![allow(non_camel_case_types)]
+
+use core::ffi::{c_int, c_void};
+use std::sync::Arc;
+
+#[repr(C)]
+pub struct enet_crc_iov {
+    pub data: *const u8,
+    pub len: usize,
+}
+
+#[repr(C)]
+pub struct enet_crc_ctx {
+    _private: [u8; 0],
+}
+
+pub const ENET_CRC_OK: c_int = 0;
+
+extern "C" {
+    pub fn enet_crc_abi_version() -> c_int;
+    pub fn enet_crc_strerror(status: c_int) -> *const core::ffi::c_char;
+    pub fn enet_crc_last_hip_error() -> c_int;
+    pub fn enet_crc_device_count() -> c_int;
+    pub fn enet_crc_ctx_create(device: c_int, out_ctx: *mut *mut enet_crc_ctx) -> c_int;
+    pub fn enet_crc_ctx_destroy(ctx: *mut enet_crc_ctx);
+    pub fn enet_crc32_iov(ctx: *mut enet_crc_ctx, bufs: *const enet_crc_iov, nbufs: usize, out_crc: *mut u32) -> c_int;
+    pub fn enet_crc32_uniform_device(d_base: *const c_void, stride: u64, length: u32, count: u64,
+                                     d_out: *mut u32, hip_stream: *mut c_void) -> c_int;
+    pub fn enet_crc32_ragged_device(d_base: *const c_void, d_offsets: *const u64, d_lengths: *const u32,
+                                    count: u64, d_out: *mut u32, hip_stream: *mut c_void) -> c_int;
+    pub fn enet_crc32_ragged_host(ctx: *mut enet_crc_ctx, h_base: *const c_void, h_offsets: *const u64,
+                                  h_lengths: *const u32, count: u64, h_out: *mut u32) -> c_int;
+}
+
+#[derive(Debug, Clone, Copy, PartialEq, Eq)]
+pub struct CrcError {
+    pub status: i32,
+    pub hip_error: i32,
+}
+
+struct Ctx(*mut enet_crc_ctx);
+// The C ABI serialises calls on one context with an internal lock.
+unsafe impl Send for Ctx {}
+unsafe impl Sync for Ctx {}
+impl Drop for Ctx {
+    fn drop(&mut self) {
+        unsafe { enet_crc_ctx_destroy(self.0) }
+    }
+}
+
+/// A device context; cheap to clone (shared).
+#[derive(Clone)]
+pub struct GpuCrc32 {
+    ctx: Arc<Ctx>,
+}
+
+impl GpuCrc32 {
+    pub fn new(device: i32) -> Result<Self, CrcError> {
+        let mut p = core::ptr::null_mut();
+        let st = unsafe { enet_crc_ctx_create(device, &mut p) };
+        if st != ENET_CRC_OK {
+            return Err(CrcError { status: st, hip_error: unsafe { enet_crc_last_hip_error() } });
+        }
+        Ok(Self { ctx: Arc::new(Ctx(p)) })
+    }
+
+    /// Same contract as `rusty_enet::crc32` (src/crc32.rs:39), but fallible.
+    pub fn crc32(&self, in_buffers: &[&[u8]]) -> Result<u32, CrcError> {
+        let iov: Vec<enet_crc_iov> =
+            in_buffers.iter().map(|b| enet_crc_iov { data: b.as_ptr(), len: b.len() }).collect();
+        let mut out = 0u32;
+        let st = unsafe { enet_crc32_iov(self.ctx.0, iov.as_ptr(), iov.len(), &mut out) };
+        if st != ENET_CRC_OK {
+            return Err(CrcError { status: st, hip_error: unsafe { enet_crc_last_hip_error() } });
+        }
+        Ok(out)
+    }
+
+    /// The value for `HostSettings::checksum`.  The reference hook cannot
+    /// fail, so a device error panics (fail loudly; there is no CPU fallback).
+    pub fn checksum_fn(&self) -> Box<dyn Fn(&[&[u8]]) -> u32> {
+        let me = self.clone();
+        Box::new(move |bufs: &[&[u8]]| me.crc32(bufs).expect("enet_crc_amd: GPU checksum failed"))
+    }
+
+    /// Host-resident batch: one checksum per (offset, length) packet of `data`.
+    pub fn crc32_ragged_host(&self, data: &[u8], offsets: &[u64], lengths: &[u32]) -> Result<Vec<u32>, CrcError> {
+        assert_eq!(offsets.len(), lengths.len());
+        for (o, l) in offsets.iter().zip(lengths) {
+            assert!(*o as usize + *l as usize <= data.len(), "packet out of bounds");
+        }
+        let mut out = vec![0u32; offsets.len()];
+        let st = unsafe {
+            enet_crc32_ragged_host(self.ctx.0, data.as_ptr().cast(), offsets.as_ptr(), lengths.as_ptr(),
+                                   offsets.len() as u64, out.as_mut_ptr())
+        };
+        if st != ENET_CRC_OK {
+            return Err(CrcError { status: st, hip_error: unsafe { enet_crc_last_hip_error() } });
+        }
+        Ok(out)
+    }
+}
+
+#[cfg(test)]
+mod test {
+    // The reference's own known answers, src/crc32.rs:49-57.
+    #[test]
+    fn crc32() {
+        let gpu = super::GpuCrc32::new(0).unwrap();
+        assert_eq!(gpu.crc32(&[&[1, 2, 3, 4, 5, 6, 7, 8]]).unwrap(), 3314076223);
+        assert_eq!(gpu.crc32(&[&[1, 2, 3, 4, 5, 6, 7, 8], &[8, 7, 6, 5, 4, 3, 2, 1]]).unwrap(), 1712484799);
+    }
+}
