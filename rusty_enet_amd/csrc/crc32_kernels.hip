@@ -1,43 +1,57 @@
 // CDNA4 (gfx950) kernels for the ENet per-datagram CRC-32.
 //
 // Reference: jabuwu/rusty_enet src/crc32.rs:39-47 (one serial Sarwate chain per
-// call).  Here every packet of a batch is checksummed by a GROUP of G lanes of a
-// wavefront; a wave holds 64/G packets at once.
+// call, one call per datagram from src/c/protocol.rs:1499 / :2287).  Here a batch
+// of packets is checksummed in one launch; a GROUP of 8 lanes cooperates on one
+// packet and a wavefront holds 8 packets at a time (a "round").
 //
-// Per packet (DESIGN.md §3 has the derivation):
-//   * The packet's bytes [s, e) are viewed as little-endian 32-bit words on the
-//     4-byte grid that ends at a1 = e & ~3.  Word d (d = 1 is the last) lives at
-//     a1 - 4d.  The zero-initialised register after the words is
-//         R = XOR_d M32^d (w_d),  M32 = "advance over 32 zero bits".
-//   * Chunk c (16 bytes, words d = 4c+4 .. 4c+1) belongs to lane k = c mod G.
-//     Each of the lane's four word slots is an independent Horner stream with
-//     step W = 4G words:  h <- M32^W(h) ^ w.  One replicated LDS operator table
-//     (M32^W) serves every step; the first (top) step needs no lookup.
-//   * Bytes before s in the top word are masked off and the 0xFFFFFFFF initial
-//     register is injected by XOR-ing head_k[s & 3] into that word.
-//   * Combine: in-lane Horner with M32 over the four slots, then a log2(G)
-//     level DPP/shuffle tree with fixed shifts M32^(4*2^l), then one M32.  All
-//     shifts are fixed, so no variable-distance GF(2) multiply is ever needed.
-//   * Trailing e & 3 bytes: Sarwate steps (src/crc32.rs:43) on lane 0.
-//   * Output: bswap32(~R)  ==  (!crc).to_be()  (src/crc32.rs:46).
+// Arithmetic (DESIGN.md §3 has the derivation; tests/cpp/kernel_sim.cpp models it):
+//   * The packet is viewed as little-endian 32-bit words on the 4-byte grid that
+//     ends at a1 = e & ~3 (crc32_geometry.hpp).  Word d (d = 1 is the last) sits
+//     at a1 - 4d; the zero-initialised register after the words is
+//         R = XOR_d M32^d (w_d),   M32 = "advance the register over 32 zero bits".
+//   * 16-byte chunk c (counted from the end) belongs to lane k = c % 8 at step
+//     i = c / 8.  Each lane's 4 word slots are independent Horner streams with
+//     step W = 32 words:  h <- M32^32(h) ^ w, through one replicated LDS table.
+//     Steps before a packet's top chunk read zeros and leave h = 0.
+//   * The top word is masked to the packet's own bytes and the 0xFFFFFFFF initial
+//     register is injected by XOR-ing head_k[s & 3] into it.
+//   * Round end: in-lane Horner with M32 over the 4 slots, a 3-level DPP tree
+//     with fixed shifts M32^4/8/16 across the 8 lanes, one more M32, then Sarwate
+//     byte steps for the e & 3 trailing bytes (src/crc32.rs:43) and
+//     bswap32(~R) == (!crc).to_be() (src/crc32.rs:46).
+//
+// Memory pipeline.  Every slot issues exactly one global_load_dwordx4 per lane,
+// unconditionally: chunks outside a packet read a zero dummy, so control flow
+// between a load and its use is straight-line and hipcc's s_waitcnt counts stay
+// exact (no vmcnt(0) drains; see DESIGN.md "waitcnt discipline").
+//   crc32_rounds_kernel<NS>: every packet has NS-1..NS steps (uniform batches, or
+//     length-bucketed ragged batches).  One loop iteration = one round: consume
+//     round r's NS slots while issuing round r+1's NS loads into the same ring
+//     registers; descriptors are prefetched two rounds ahead.
+//   crc32_stream_kernel<U>: any lengths.  A round is padded to a multiple of U
+//     slots and streamed through a U-deep ring; only round boundaries drain.
 //
 // LDS (one 1024-thread workgroup per CU, 144 KiB):
-//   [0, 128 KiB)  M32^W tables, replicated 32x so that lane l always reads bank
-//                 l%32 (conflict-free ds_read_b32).  Table k, entry i, bank b at
-//                 dword (k>>1)*16384 + i*64 + (k&1)*32 + b.  The byte address is
-//                 built with ONE v_perm_b32: byte1 = register byte k, byte0 =
-//                 lane*4, byte2 = table pair.
-//   [128 KiB, +) unreplicated small operators: M32^1 (set 0) and the tree
-//                 operators M32^(4*2^(l-1)) (set l).
+//   [0, 128 KiB)  M32^32 tables replicated 32x: lane l always reads bank l%32,
+//                 conflict-free ds_read_b32.  Table t, entry i, bank b at dword
+//                 (t>>1)*16384 + i*64 + (t&1)*32 + b; the byte address is ONE
+//                 v_perm_b32 (byte1 = register byte t, byte0 = lane*4, byte2 = pair).
+//   [128 KiB, +)  unreplicated: M32^1 (set 0), tree operators M32^4/8/16 (sets 1..3).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "crc32_ops.hpp"
+#include <utility>
+
+#include "crc32_geometry.hpp"
 #include "crc32_kernels.hpp"
+#include "crc32_ops.hpp"
 
 namespace enet_crc {
 
 __device__ const OpTables g_op_tables = kOpTables;
+// Read by every lane whose chunk lies outside its packet; never written.
+__device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
 
 namespace {
 
@@ -47,33 +61,25 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct __attribute__((packed, aligned(4))) U32x4A4 {
   u32x4 v;
 };
-
-constexpr int kBlock = 1024;
-constexpr int kWavesPerBlock = kBlock / 64;
-constexpr uint32_t kMainDwords = 32768;  // 4 tables x 256 entries x 32 banks
-
-constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
-
-template <int G>
-struct Layout {
-  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "lanes per packet");
-  static constexpr int kStreams = 4 * G;         // words per group step
-  static constexpr int kMainLevel = ilog2(kStreams);
-  static constexpr int kTreeLevels = ilog2(G);
-  static constexpr int kSmallSets = 1 + kTreeLevels;
-  static constexpr uint32_t kLdsDwords = kMainDwords + kSmallSets * 1024;
-  static_assert(kMainLevel < kOpLevels, "operator table level");
-};
-
-// Global-address-space loads from integer addresses (keeps them global_load_*,
-// not flat_*: flat loads also count on lgkmcnt and would serialise with the
-// LDS table lookups).
+// Global address space: keeps loads global_load_* (flat_* would also count on
+// lgkmcnt and serialise against the LDS table lookups).
 typedef __attribute__((address_space(1))) const uint32_t GlobalU32;
 typedef __attribute__((address_space(1))) const U32x4A4 GlobalU32x4A4;
 
-__device__ __forceinline__ uint32_t load_word(uintptr_t addr) {
-  return *reinterpret_cast<GlobalU32*>(addr);
-}
+constexpr int kBlock = 1024;
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int G = kLanesPerPacket;
+constexpr uint32_t kMainDwords = 32768;  // 4 tables x 256 entries x 32 banks
+
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
+constexpr int kMainLevel = ilog2(4 * G);  // M32^(4G) = M32^32
+constexpr int kTreeLevels = ilog2(G);
+constexpr int kSmallSets = 1 + kTreeLevels;
+constexpr uint32_t kLdsDwords = kMainDwords + kSmallSets * 1024;
+static_assert(kMainLevel < kOpLevels, "operator level");
+
+__device__ __forceinline__ uint32_t load_word(uint64_t addr) { return *reinterpret_cast<GlobalU32*>(addr); }
+__device__ __forceinline__ u32x4 load_chunk(uint64_t addr) { return reinterpret_cast<GlobalU32x4A4*>(addr)->v; }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -83,18 +89,14 @@ __device__ __forceinline__ uint32_t lds_at(const uint32_t* lds, uint32_t byte_ad
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
 }
 
-// h' = M32^W(h) ^ w through the replicated tables.  lp0 = lane*4, lp1 = lane*4 | 64 KiB.
-__device__ __forceinline__ uint32_t horner_main(const uint32_t* lds, uint32_t h, uint32_t w,
-                                                uint32_t lp0, uint32_t lp1) {
+// h' = M32^32(h) ^ w through the replicated tables.  lp0 = lane*4, lp1 = lane*4 | 64 KiB.
+__device__ __forceinline__ uint32_t horner_main(const uint32_t* lds, uint32_t h, uint32_t w, uint32_t lp0,
+                                                uint32_t lp1) {
   const uint32_t a0 = __builtin_amdgcn_perm(h, lp0, 0x0C020400u);
   const uint32_t a1 = __builtin_amdgcn_perm(h, lp0, 0x0C020500u);
   const uint32_t a2 = __builtin_amdgcn_perm(h, lp1, 0x0C020600u);
   const uint32_t a3 = __builtin_amdgcn_perm(h, lp1, 0x0C020700u);
-  const uint32_t t0 = lds_at(lds, a0);
-  const uint32_t t1 = lds_at(lds, a1 + 128u);
-  const uint32_t t2 = lds_at(lds, a2);
-  const uint32_t t3 = lds_at(lds, a3 + 128u);
-  return xor3(xor3(t0, t1, t2), t3, w);
+  return xor3(xor3(lds_at(lds, a0), lds_at(lds, a1 + 128u), lds_at(lds, a2)), lds_at(lds, a3 + 128u), w);
 }
 
 // M32^n(x) through an unreplicated 4x256 table set.
@@ -103,159 +105,331 @@ __device__ __forceinline__ uint32_t apply_small(const uint32_t* set, uint32_t x)
          set[768 + (x >> 24)];
 }
 
+// Lane l receives lane l+d of its 16-lane DPP row (groups of 8 never straddle a row).
+template <int d>
+__device__ __forceinline__ uint32_t from_lane_plus(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + d, 0xF, 0xF, true);
+}
+
 __device__ __forceinline__ uint32_t head_k(uint32_t v) {
   return v == 0 ? kOpTables.head_k[0]
                 : (v == 1 ? kOpTables.head_k[1] : (v == 2 ? kOpTables.head_k[2] : kOpTables.head_k[3]));
 }
 
-template <int G>
+__device__ __forceinline__ int32_t wave_max_over_groups(int32_t v) {
+  int32_t m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+  for (int g = 1; g < kPacketsPerWave; ++g) m = max(m, __builtin_amdgcn_readlane(v, g * G));
+  return m;
+}
+
 __device__ __forceinline__ void fill_lds(uint32_t* lds) {
-  using L = Layout<G>;
-  const int t = threadIdx.x;  // (table k, entry i) pairs: 4 x 256 = kBlock
+  const int t = threadIdx.x;  // (table, entry) pairs: 4 x 256 = kBlock
   {
-    const int k = t >> 8, i = t & 255;
-    const uint32_t v = g_op_tables.op[L::kMainLevel][k][i];
+    const int tab = t >> 8, i = t & 255;
+    const uint32_t v = g_op_tables.op[kMainLevel][tab][i];
     const u32x4 vv = {v, v, v, v};
-    u32x4* dst = reinterpret_cast<u32x4*>(lds + (k >> 1) * 16384 + i * 64 + (k & 1) * 32);
+    u32x4* dst = reinterpret_cast<u32x4*>(lds + (tab >> 1) * 16384 + i * 64 + (tab & 1) * 32);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dst[j] = vv;
   }
-  for (int x = t; x < L::kSmallSets * 1024; x += kBlock) {
+  for (int x = t; x < kSmallSets * 1024; x += kBlock) {
     const int set = x >> 10, rem = x & 1023;
-    const int level = set == 0 ? 0 : set + 1;
+    const int level = set == 0 ? 0 : set + 1;  // M32^1, then M32^(4*2^(set-1))
     lds[kMainDwords + x] = g_op_tables.op[level][rem >> 8][rem & 255];
   }
 }
 
-template <int G>
-__device__ __forceinline__ u32x4 load_chunk(uintptr_t a1, uint32_t k, int64_t i) {
-  const uintptr_t addr = a1 - 16u * (uintptr_t)(k + (uint64_t)G * (uint64_t)i + 1u);
-  return reinterpret_cast<GlobalU32x4A4*>(addr)->v;
-}
+template <bool kRagged>
+struct Batch {
+  uint64_t base;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
+  uint64_t stride;
+  uint32_t length;
+  uint64_t count;
+};
 
-// CRC register (before finalisation) of bytes [sa, ea) for the group's lane k.
-// Valid on lane k == 0 only.
-template <int G>
-__device__ __forceinline__ uint32_t group_crc_register(const uint32_t* lds, uintptr_t sa, uintptr_t ea,
-                                                       uint32_t k, uint32_t lp0, uint32_t lp1) {
-  using L = Layout<G>;
-  const uintptr_t top = sa & ~(uintptr_t)3;
-  const uintptr_t a1 = ea & ~(uintptr_t)3;
-  const uint64_t nwords = (uint64_t)(a1 - top) >> 2;
-  uint32_t reg = kInitRegister;
-  if (nwords > 0) {
-    const uint64_t nchunks = (nwords + 3) >> 2;
-    const int64_t nsteps = (int64_t)((nchunks + G - 1) / G);
-    uint32_t h0, h1, h2, h3;
-    {  // top step: may start before sa; per-word loads with masking
-      const int64_t c = (int64_t)k + (int64_t)G * (nsteps - 1);
-      const int64_t rel0 = (int64_t)(a1 - top) - 16 * (c + 1);
-      uint32_t w[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t rel = rel0 + 4 * j;
-        uint32_t x = 0;
-        if (rel >= 0) x = load_word(top + (uintptr_t)rel);
-        if (rel == 0) {
-          const uint32_t v = (uint32_t)(sa - top);
-          x = (x & (0xFFFFFFFFu << (8 * v))) ^ head_k(v);
-        }
-        w[j] = x;
-      }
-      h0 = w[0]; h1 = w[1]; h2 = w[2]; h3 = w[3];
-    }
-    // Remaining steps: whole 16-byte chunks, three loads in flight per lane.
-    int64_t i = nsteps - 2;
-    u32x4 q0 = {0, 0, 0, 0}, q1 = {0, 0, 0, 0}, q2 = {0, 0, 0, 0};
-    if (i >= 0) q0 = load_chunk<G>(a1, k, i);
-    if (i >= 1) q1 = load_chunk<G>(a1, k, i - 1);
-    if (i >= 2) q2 = load_chunk<G>(a1, k, i - 2);
-    while (i >= 0) {
-      h0 = horner_main(lds, h0, q0.x, lp0, lp1);
-      h1 = horner_main(lds, h1, q0.y, lp0, lp1);
-      h2 = horner_main(lds, h2, q0.z, lp0, lp1);
-      h3 = horner_main(lds, h3, q0.w, lp0, lp1);
-      if (i >= 3) q0 = load_chunk<G>(a1, k, i - 3);
-      if (--i < 0) break;
-      h0 = horner_main(lds, h0, q1.x, lp0, lp1);
-      h1 = horner_main(lds, h1, q1.y, lp0, lp1);
-      h2 = horner_main(lds, h2, q1.z, lp0, lp1);
-      h3 = horner_main(lds, h3, q1.w, lp0, lp1);
-      if (i >= 3) q1 = load_chunk<G>(a1, k, i - 3);
-      if (--i < 0) break;
-      h0 = horner_main(lds, h0, q2.x, lp0, lp1);
-      h1 = horner_main(lds, h1, q2.y, lp0, lp1);
-      h2 = horner_main(lds, h2, q2.z, lp0, lp1);
-      h3 = horner_main(lds, h3, q2.w, lp0, lp1);
-      if (i >= 3) q2 = load_chunk<G>(a1, k, i - 3);
-      --i;
-    }
-    // Combine the 4G streams.
-    const uint32_t* m1 = lds + kMainDwords;
-    uint32_t y = apply_small(m1, h0) ^ h1;
-    y = apply_small(m1, y) ^ h2;
-    y = apply_small(m1, y) ^ h3;
-#pragma unroll
-    for (int l = 1; l <= L::kTreeLevels; ++l) {
-      const uint32_t t = apply_small(lds + kMainDwords + l * 1024, y);
-      y ^= (uint32_t)__shfl_down((int)t, 1 << (l - 1), G);
-    }
-    reg = apply_small(m1, y);
+// Descriptor of packet p (p >= count reads as an empty packet at offset 0).
+template <bool kRagged>
+__device__ __forceinline__ void load_desc(const Batch<kRagged>& b, uint64_t p, uint64_t& off, uint32_t& len) {
+  if constexpr (kRagged) {
+    const uint64_t q = p < b.count ? p : b.count - 1;
+    off = b.offsets[q];
+    len = p < b.count ? b.lengths[q] : 0;
+  } else {
+    off = (p < b.count ? p : 0) * b.stride;
+    len = p < b.count ? b.length : 0;
   }
-  return reg;
 }
 
-// Sarwate steps over the trailing (< 4) bytes [max(a1, sa), ea): src/crc32.rs:43.
-__device__ __forceinline__ uint32_t tail_bytes(const uint32_t* sarwate, uint32_t reg, uintptr_t sa,
-                                               uintptr_t ea) {
-  const uintptr_t a1 = ea & ~(uintptr_t)3;
-  const uintptr_t ts = a1 > sa ? a1 : sa;
-  if (ts < ea) {
-    const uint32_t w = load_word(a1);
-    for (uintptr_t b = ts; b < ea; ++b) {
-      const uint32_t byte = (w >> (8u * (uint32_t)(b - a1))) & 0xffu;
-      reg = (reg >> 8) ^ sarwate[(reg ^ byte) & 0xffu];
-    }
+// Round-constant slot metadata for one lane (bit layout private to this file).
+constexpr uint32_t kMetaHeadMask = 0x7;       // c != 0: top word at word index 4 - c of the top chunk
+constexpr uint32_t kMetaVShift = 3;           // 2 bits: sa - top
+constexpr uint32_t kMetaEmpty = 1u << 5;      // packet has no grid word: register = init
+constexpr uint32_t kMetaNTailShift = 6;       // 2 bits: trailing bytes (0..3)
+constexpr uint32_t kMetaTShiftShift = 8;      // 2 bits: first trailing byte's position in its word
+constexpr uint32_t kMetaStore = 1u << 10;     // packet index < count
+constexpr uint32_t kMetaFallback = 1u << 11;  // top chunk begins before the caller's buffer
+
+__device__ __forceinline__ uint32_t round_meta(const PacketGeo& g, uint32_t k, uint64_t base4, bool store,
+                                               uint64_t& tail_addr, uint64_t dummy) {
+  uint32_t head = 0, fb = 0;
+  if (g.nsteps > 0) {
+    const int32_t itop = g.nsteps - 1;
+    const int64_t rel0 = chunk_offset(g, k, itop, g.top);
+    head = (rel0 > -16 && rel0 <= 0) ? (uint32_t)(rel0 / 4 + 4) : 0u;
+    fb = chunk_kind(g, k, itop, base4) == kChunkFallback ? kMetaFallback : 0u;
   }
-  return reg;
+  const uint64_t ts = g.a1 > g.sa ? g.a1 : g.sa;
+  const uint32_t ntail = (uint32_t)(g.ea - ts);
+  tail_addr = ntail ? g.a1 : dummy;
+  return head | ((uint32_t)(g.sa - g.top) << kMetaVShift) | (g.nsteps == 0 ? kMetaEmpty : 0u) |
+         (ntail << kMetaNTailShift) | ((uint32_t)(ts - g.a1) << kMetaTShiftShift) | (store ? kMetaStore : 0u) | fb;
 }
 
-template <int G, bool kRagged>
-__global__ __launch_bounds__(kBlock) void crc32_packets_kernel(const uint8_t* __restrict__ base,
-                                                              const uint64_t* __restrict__ offsets,
-                                                              const uint32_t* __restrict__ lengths,
-                                                              uint64_t stride, uint32_t length,
-                                                              uint64_t count, uint32_t* __restrict__ out) {
-  using L = Layout<G>;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[L::kLdsDwords];
-  fill_lds<G>(lds);
-  __syncthreads();
+// Top chunk words: keep only the packet's own bytes and inject the initial register.
+__device__ __forceinline__ void mask_top(uint32_t meta, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) {
+  const uint32_t head = meta & kMetaHeadMask;
+  const uint32_t v = (meta >> kMetaVShift) & 3u;
+  const uint32_t keep = 0xFFFFFFFFu << (8u * v), kk = head_k(v);
+  const int32_t j0 = 4 - (int32_t)head;  // word index of the top word
+  w0 = j0 > 0 ? 0 : (j0 == 0 ? (w0 & keep) ^ kk : w0);
+  w1 = j0 > 1 ? 0 : (j0 == 1 ? (w1 & keep) ^ kk : w1);
+  w2 = j0 > 2 ? 0 : (j0 == 2 ? (w2 & keep) ^ kk : w2);
+  w3 = j0 == 3 ? (w3 & keep) ^ kk : w3;
+}
 
+// Fallback for a top chunk that begins before the caller's buffer: read only the
+// words at or after the chunk's top word (rare: packets within 12 bytes of base).
+// One asm statement issues the loads AND waits for them, so hipcc sees a plain
+// definition of w0..w3: no pending load on this rare path can leak into the waitcnt
+// bookkeeping of the ring registers (which would turn every slot's wait into a
+// vmcnt(0) drain).
+__device__ __forceinline__ void load_top_words(uint64_t chunk_addr, uint32_t meta, uint64_t dummy, uint32_t& w0,
+                                               uint32_t& w1, uint32_t& w2, uint32_t& w3) {
+  const int32_t j0 = 4 - (int32_t)(meta & kMetaHeadMask);
+  const uint64_t a0 = j0 <= 0 ? chunk_addr : dummy;
+  const uint64_t a1 = j0 <= 1 ? chunk_addr + 4 : dummy;
+  const uint64_t a2 = j0 <= 2 ? chunk_addr + 8 : dummy;
+  const uint64_t a3 = chunk_addr + 12;
+  asm volatile(
+      "global_load_dword %0, %4, off\n\t"
+      "global_load_dword %1, %5, off\n\t"
+      "global_load_dword %2, %6, off\n\t"
+      "global_load_dword %3, %7, off\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(w0), "=&v"(w1), "=&v"(w2), "=&v"(w3)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
+      : "memory");
+}
+
+// Round end: combine the 4x8 streams, trailing bytes, store (lane 0 of the group).
+__device__ __forceinline__ void finish_round(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                             uint32_t meta, uint32_t tail_word, uint32_t k, uint32_t* dst) {
+  const uint32_t* m1 = lds + kMainDwords;
+  uint32_t y = apply_small(m1, h0) ^ h1;
+  y = apply_small(m1, y) ^ h2;
+  y = apply_small(m1, y) ^ h3;
+  y ^= from_lane_plus<1>(apply_small(lds + kMainDwords + 1024, y));
+  y ^= from_lane_plus<2>(apply_small(lds + kMainDwords + 2048, y));
+  y ^= from_lane_plus<4>(apply_small(lds + kMainDwords + 3072, y));
+  uint32_t reg = apply_small(m1, y);
+  if (meta & kMetaEmpty) reg = kInitRegister;
+  const uint32_t ntail = (meta >> kMetaNTailShift) & 3u;
+  const uint32_t tsh = (meta >> kMetaTShiftShift) & 3u;
+  const uint32_t* sarwate = lds + kMainDwords + 768;  // M32(b << 24) == CRC table
+#pragma unroll
+  for (uint32_t t = 0; t < 3; ++t) {
+    if (t < ntail) reg = (reg >> 8) ^ sarwate[(reg ^ (tail_word >> (8u * (tsh + t)))) & 0xffu];
+  }
+  if (k == 0 && (meta & kMetaStore)) *dst = __builtin_bswap32(~reg);
+}
+
+// Ring loads must issue in slot order: hipcc's scheduler otherwise reorders the
+// independent loads of a loop body (it reversed them), the ring order breaks, and the
+// loop-header merge of the waitcnt scoreboard degrades every slot's wait to vmcnt(1).
+__device__ __forceinline__ void issue_order_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+struct LaneConsts {
+  uint32_t k, grp, lp0, lp1;
+  uint64_t base4, dummy;
+};
+
+__device__ __forceinline__ LaneConsts lane_consts(uint64_t base) {
+  LaneConsts c;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t k = lane & (G - 1);
-  const uint32_t lp0 = (lane & 31u) << 2;
-  const uint32_t lp1 = lp0 | 0x10000u;
-  const uint32_t* sarwate = lds + kMainDwords + 768;  // op[0] table 3 == CRC table
-  constexpr uint64_t kGroupsPerWave = 64 / G;
-  const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const uint64_t total_groups = (uint64_t)gridDim.x * kWavesPerBlock * kGroupsPerWave;
+  c.k = lane & (G - 1);
+  c.grp = lane / G;
+  c.lp0 = (lane & 31u) << 2;
+  c.lp1 = c.lp0 | 0x10000u;
+  c.base4 = base & ~(uint64_t)3;
+  c.dummy = (uint64_t)(uintptr_t)g_zero_chunk;
+  return c;
+}
 
-  for (uint64_t p = wave * kGroupsPerWave + lane / G; p < count; p += total_groups) {
-    uint64_t s, len;
-    if constexpr (kRagged) {
-      s = offsets[p];
-      len = lengths[p];
-    } else {
-      s = p * stride;
-      len = length;
+// ---------------------------------------------------------------------------------
+// Round kernel: every packet of the launch has at most NS steps.
+// ---------------------------------------------------------------------------------
+template <int NS>
+struct RoundPlan {
+  uint64_t base;       // this lane's chunk address at slot 0 (step NS-1)
+  uint32_t vmask;      // bit s: slot s reads real data
+  uint32_t meta;       // round_meta()
+  int32_t top_slot;    // slot of the group's top step (NS: none)
+  uint64_t tail_addr;  // word holding the trailing bytes, or the dummy
+};
+
+template <int NS>
+__device__ __forceinline__ RoundPlan<NS> plan_round(const PacketGeo& g, const LaneConsts& c, bool store) {
+  RoundPlan<NS> pl;
+  pl.base = g.a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (NS - 1);
+  pl.meta = round_meta(g, c.k, c.base4, store, pl.tail_addr, c.dummy);
+  pl.top_slot = NS - g.nsteps;  // g.nsteps <= NS by the launch contract
+  uint32_t vm = 0;
+  if (g.nsteps > 0) {
+    const int kind = chunk_kind(g, c.k, g.nsteps - 1, c.base4);
+    vm = ((1u << NS) - 1u) & ~((2u << pl.top_slot) - 1u);  // slots after the top one
+    if (kind == kChunkDirect) vm |= 1u << pl.top_slot;
+  }
+  pl.vmask = vm;
+  return pl;
+}
+
+template <int NS>
+__device__ __forceinline__ uint64_t slot_addr(const RoundPlan<NS>& pl, int s, uint64_t dummy) {
+  return (pl.vmask >> s) & 1u ? pl.base + (uint64_t)kBytesPerStep * s : dummy;
+}
+
+template <int NS, bool kRagged>
+__global__ __launch_bounds__(kBlock) void crc32_rounds_kernel(Batch<kRagged> b, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(b.base);
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  const uint64_t first = (uint64_t)wave * kPacketsPerWave;
+  const uint64_t P = (uint64_t)gridDim.x * kWavesPerBlock * kPacketsPerWave;
+  if (first >= b.count) return;
+  const uint64_t nrounds = (b.count - first + P - 1) / P;
+
+  uint64_t d_off;
+  uint32_t d_len;
+  load_desc(b, first + c.grp, d_off, d_len);
+  RoundPlan<NS> cur = plan_round<NS>(make_geo(b.base + d_off, d_len), c, first + c.grp < b.count);
+  load_desc(b, first + P + c.grp, d_off, d_len);  // round 1, consumed one iteration later
+
+  u32x4 q[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    q[s] = load_chunk(slot_addr(cur, s, c.dummy));
+    issue_order_fence();
+  }
+  uint32_t tw_cur = load_word(cur.tail_addr);
+
+  for (uint64_t r = 0; r < nrounds; ++r) {
+    // Producer side: plan round r+1 and prefetch round r+2's descriptor.
+    const uint64_t pn = first + (r + 1) * P + c.grp;
+    const RoundPlan<NS> nxt = plan_round<NS>(make_geo(b.base + d_off, d_len), c, pn < b.count);
+    load_desc(b, pn + P, d_off, d_len);
+
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint32_t w0 = q[s].x, w1 = q[s].y, w2 = q[s].z, w3 = q[s].w;
+      const bool top = s == cur.top_slot;
+      if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+        if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
+          if (top && (cur.meta & kMetaFallback))
+            load_top_words(cur.base + (uint64_t)kBytesPerStep * s, cur.meta, c.dummy, w0, w1, w2, w3);
+        }
+        if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
+      }
+      if (s == 0) {  // M32^32(0) = 0: the first step needs no lookups
+        h0 = w0; h1 = w1; h2 = w2; h3 = w3;
+      } else {
+        h0 = horner_main(lds, h0, w0, c.lp0, c.lp1);
+        h1 = horner_main(lds, h1, w1, c.lp0, c.lp1);
+        h2 = horner_main(lds, h2, w2, c.lp0, c.lp1);
+        h3 = horner_main(lds, h3, w3, c.lp0, c.lp1);
+      }
+      q[s] = load_chunk(slot_addr(nxt, s, c.dummy));
+      issue_order_fence();
     }
-    const uintptr_t sa = (uintptr_t)base + s;
-    const uintptr_t ea = sa + len;
-    uint32_t reg = group_crc_register<G>(lds, sa, ea, k, lp0, lp1);
-    if (k == 0) {
-      reg = tail_bytes(sarwate, reg, sa, ea);
-      out[p] = __builtin_bswap32(~reg);
+    const uint32_t tw_next = load_word(nxt.tail_addr);
+    finish_round(lds, h0, h1, h2, h3, cur.meta, tw_cur, c.k, out + (first + r * P + c.grp));
+    cur = nxt;
+    tw_cur = tw_next;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Streaming kernel: any packet lengths.  Each round (8 packets of a wave) is padded
+// to T = ceil(max nsteps / U) * U slots and streamed through a U-deep ring.
+// ---------------------------------------------------------------------------------
+template <int U, bool kRagged>
+__global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(b.base);
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  const uint64_t first = (uint64_t)wave * kPacketsPerWave;
+  const uint64_t P = (uint64_t)gridDim.x * kWavesPerBlock * kPacketsPerWave;
+  if (first >= b.count) return;
+  const uint64_t nrounds = (b.count - first + P - 1) / P;
+
+  for (uint64_t r = 0; r < nrounds; ++r) {
+    const uint64_t p = first + r * P + c.grp;
+    uint64_t off;
+    uint32_t len;
+    load_desc(b, p, off, len);
+    const PacketGeo g = make_geo(b.base + off, len);
+    uint64_t tail_addr;
+    const uint32_t meta = round_meta(g, c.k, c.base4, p < b.count, tail_addr, c.dummy);
+    const uint32_t tail_word = load_word(tail_addr);
+    const int32_t iters = (wave_max_over_groups(g.nsteps) + U - 1) / U;
+    const int32_t nslots = iters * U;
+    // Slot j reads step i = nslots-1-j; this lane's chunk at step i is
+    // a1 - 16(k+1) - 128 i: real data for i < nsteps-1 (and i = nsteps-1 when direct).
+    const uint64_t base = g.a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(nslots - 1);
+    const int32_t top_slot = nslots - g.nsteps;  // == nslots when the packet is empty
+    const bool top_direct = g.nsteps > 0 && chunk_kind(g, c.k, g.nsteps - 1, c.base4) == kChunkDirect;
+    auto addr_of = [&](int32_t j) -> uint64_t {
+      const bool real = j > top_slot || (j == top_slot && top_direct);
+      return real ? base + (uint64_t)kBytesPerStep * (uint64_t)j : c.dummy;
+    };
+    u32x4 q[U];
+#pragma unroll
+    for (int s = 0; s < U; ++s) {
+      q[s] = load_chunk(addr_of(s));
+      issue_order_fence();
     }
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    for (int32_t it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int s = 0; s < U; ++s) {
+        const int32_t j = it * U + s;
+        uint32_t w0 = q[s].x, w1 = q[s].y, w2 = q[s].z, w3 = q[s].w;
+        const bool top = j == top_slot;
+        if (__builtin_amdgcn_ballot_w64(top && (meta & kMetaHeadMask))) {
+          if (__builtin_amdgcn_ballot_w64(top && (meta & kMetaFallback))) {
+            if (top && (meta & kMetaFallback))
+              load_top_words(base + (uint64_t)kBytesPerStep * (uint64_t)j, meta, c.dummy, w0, w1, w2, w3);
+          }
+          if (top && (meta & kMetaHeadMask)) mask_top(meta, w0, w1, w2, w3);
+        }
+        h0 = horner_main(lds, h0, w0, c.lp0, c.lp1);
+        h1 = horner_main(lds, h1, w1, c.lp0, c.lp1);
+        h2 = horner_main(lds, h2, w2, c.lp0, c.lp1);
+        h3 = horner_main(lds, h3, w3, c.lp0, c.lp1);
+        q[s] = load_chunk(j + U < nslots ? addr_of(j + U) : c.dummy);
+        issue_order_fence();
+      }
+    }
+    finish_round(lds, h0, h1, h2, h3, meta, tail_word, c.k, out + p);
   }
 }
 
@@ -263,29 +437,73 @@ __global__ __launch_bounds__(kBlock) void crc32_packets_kernel(const uint8_t* __
 
 int cu_count_for_current_device();
 
-template <int G, bool kRagged>
-static hipError_t launch_packets(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
-                                 uint64_t stride, uint32_t length, uint64_t count, uint32_t* out,
-                                 hipStream_t stream) {
-  if (count == 0) return hipSuccess;
+constexpr int kMaxRoundSteps = 14;  // NS 1..14 (packets up to 1792 B); NS >= 15 exceeds 128 VGPRs
+constexpr int kStreamDepth = 8;
+
+template <bool kRagged>
+struct Launcher {
+  Batch<kRagged> b;
+  uint32_t* out;
+  hipStream_t stream;
+  unsigned blocks;
+
+  template <int NS>
+  hipError_t rounds() {
+    hipLaunchKernelGGL((crc32_rounds_kernel<NS, kRagged>), dim3(blocks), dim3(kBlock), 0, stream, b, out);
+    return hipGetLastError();
+  }
+  hipError_t streaming() {
+    hipLaunchKernelGGL((crc32_stream_kernel<kStreamDepth, kRagged>), dim3(blocks), dim3(kBlock), 0, stream, b,
+                       out);
+    return hipGetLastError();
+  }
+  template <int... I>
+  hipError_t dispatch(int ns, std::integer_sequence<int, I...>) {
+    hipError_t e = hipErrorInvalidValue;
+    const bool hit = ((ns == I + 1 ? (e = rounds<I + 1>(), true) : false) || ...);
+    return hit ? e : streaming();
+  }
+};
+
+static unsigned grid_for(uint64_t count, hipError_t& err) {
   const int cus = cu_count_for_current_device();
-  if (cus <= 0) return hipErrorNoDevice;
-  constexpr uint64_t kGroupsPerBlock = (uint64_t)kWavesPerBlock * (64 / G);
-  uint64_t blocks = (count + kGroupsPerBlock - 1) / kGroupsPerBlock;
+  if (cus <= 0) {
+    err = hipErrorNoDevice;
+    return 0;
+  }
+  constexpr uint64_t kPacketsPerBlock = (uint64_t)kWavesPerBlock * kPacketsPerWave;
+  uint64_t blocks = (count + kPacketsPerBlock - 1) / kPacketsPerBlock;
   if (blocks > (uint64_t)cus) blocks = (uint64_t)cus;
-  hipLaunchKernelGGL((crc32_packets_kernel<G, kRagged>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
-                     base, offsets, lengths, stride, length, count, out);
-  return hipGetLastError();
+  err = hipSuccess;
+  return (unsigned)blocks;
 }
 
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
                           uint32_t* out, hipStream_t stream) {
-  return launch_packets<8, false>(base, nullptr, nullptr, stride, length, count, out, stream);
+  if (count == 0) return hipSuccess;
+  hipError_t err;
+  const unsigned blocks = grid_for(count, err);
+  if (err != hipSuccess) return err;
+  // Packet starts cycle through phases (base + p*stride) mod 4: steps per packet.
+  int hi = 0;
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  for (uint64_t p = 0; p < 4 && p < count; ++p) {
+    const int n = make_geo((b0 + p * stride) & 3u, length).nsteps;
+    hi = n > hi ? n : hi;
+  }
+  Launcher<false> L{Batch<false>{b0, nullptr, nullptr, stride, length, count}, out, stream, blocks};
+  if (hi >= 1 && hi <= kMaxRoundSteps) return L.dispatch(hi, std::make_integer_sequence<int, kMaxRoundSteps>{});
+  return L.streaming();
 }
 
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
                          uint64_t count, uint32_t* out, hipStream_t stream) {
-  return launch_packets<8, true>(base, offsets, lengths, 0, 0, count, out, stream);
+  if (count == 0) return hipSuccess;
+  hipError_t err;
+  const unsigned blocks = grid_for(count, err);
+  if (err != hipSuccess) return err;
+  Launcher<true> L{Batch<true>{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count}, out, stream, blocks};
+  return L.streaming();
 }
 
 }  // namespace enet_crc
