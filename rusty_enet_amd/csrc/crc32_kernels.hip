@@ -51,7 +51,7 @@ namespace enet_crc {
 
 __device__ const OpTables g_op_tables = kOpTables;
 // Read by every lane whose chunk lies outside its packet; never written.
-__device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[16] = {0};
+__device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[64] = {0};
 
 namespace {
 
@@ -224,9 +224,10 @@ __device__ __forceinline__ void load_top_words(uint64_t chunk_addr, uint32_t met
       : "memory");
 }
 
-// Round end: combine the 4x8 streams, trailing bytes, store (lane 0 of the group).
-__device__ __forceinline__ void finish_round(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
-                                             uint32_t meta, uint32_t tail_word, uint32_t k, uint32_t* dst) {
+// Combine the 4 word streams of each of the group's 8 lanes into the packet's
+// register (before trailing bytes).  Valid on lane k == 0 of the group.
+__device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
+                                                   uint32_t h3) {
   const uint32_t* m1 = lds + kMainDwords;
   uint32_t y = apply_small(m1, h0) ^ h1;
   y = apply_small(m1, y) ^ h2;
@@ -234,15 +235,26 @@ __device__ __forceinline__ void finish_round(const uint32_t* lds, uint32_t h0, u
   y ^= from_lane_plus<1>(apply_small(lds + kMainDwords + 1024, y));
   y ^= from_lane_plus<2>(apply_small(lds + kMainDwords + 2048, y));
   y ^= from_lane_plus<4>(apply_small(lds + kMainDwords + 3072, y));
-  uint32_t reg = apply_small(m1, y);
-  if (meta & kMetaEmpty) reg = kInitRegister;
-  const uint32_t ntail = (meta >> kMetaNTailShift) & 3u;
-  const uint32_t tsh = (meta >> kMetaTShiftShift) & 3u;
+  return apply_small(m1, y);
+}
+
+// Sarwate byte steps (src/crc32.rs:43) over `ntail` bytes of `word` from byte `tsh`.
+__device__ __forceinline__ uint32_t tail_steps(const uint32_t* lds, uint32_t reg, uint32_t word, uint32_t ntail,
+                                               uint32_t tsh) {
   const uint32_t* sarwate = lds + kMainDwords + 768;  // M32(b << 24) == CRC table
 #pragma unroll
   for (uint32_t t = 0; t < 3; ++t) {
-    if (t < ntail) reg = (reg >> 8) ^ sarwate[(reg ^ (tail_word >> (8u * (tsh + t)))) & 0xffu];
+    if (t < ntail) reg = (reg >> 8) ^ sarwate[(reg ^ (word >> (8u * (tsh + t)))) & 0xffu];
   }
+  return reg;
+}
+
+// Round end: combine the 4x8 streams, trailing bytes, store (lane 0 of the group).
+__device__ __forceinline__ void finish_round(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                             uint32_t meta, uint32_t tail_word, uint32_t k, uint32_t* dst) {
+  uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+  if (meta & kMetaEmpty) reg = kInitRegister;
+  reg = tail_steps(lds, reg, tail_word, (meta >> kMetaNTailShift) & 3u, (meta >> kMetaTShiftShift) & 3u);
   if (k == 0 && (meta & kMetaStore)) *dst = __builtin_bswap32(~reg);
 }
 
@@ -433,6 +445,97 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Uniform kernel: a uniform batch whose base and stride are multiples of 4, so every
+// packet has the same geometry relative to its own start.  Per-lane chunk offsets,
+// the top-chunk masks and the trailing-byte layout are computed once; a slot costs
+// exactly 4 v_perm + 4 ds_read + 2 v_bitop3 per word, slot offsets ride in the load
+// immediates, and lanes past the end of the batch re-read its last packet (valid
+// memory) without storing.  Contract (host-checked): nsteps(length) == NS, and for
+// every packet of the launch the top chunk starts at or after `lo` (the caller's
+// buffer start): the host routes the first packets that violate it through the
+// streaming kernel.
+// ---------------------------------------------------------------------------------
+struct UniformBatch {
+  uint64_t base;
+  uint64_t stride;
+  uint32_t length;
+  uint64_t count;
+};
+
+template <int NS, bool kTail>
+__global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(u.base);
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  const uint64_t first = (uint64_t)wave * kPacketsPerWave;
+  const uint64_t P = (uint64_t)gridDim.x * kWavesPerBlock * kPacketsPerWave;
+  if (first >= u.count) return;
+  const uint64_t nrounds = (u.count - first + P - 1) / P;
+
+  // Geometry of a packet starting at offset 0 (the grid word holding sa is at 0).
+  const PacketGeo g = make_geo(0, u.length);
+  const uint64_t off0 = g.a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (NS - 1);  // slot 0
+  const int64_t rel0 = (int64_t)off0;  // slot 0 is every packet's top step
+  // Slot-0 word j: keep if rel0 + 4j >= 0, inject the initial register at rel0 + 4j == 0.
+  uint32_t am[4], xm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    am[j] = rel0 + 4 * j >= 0 ? 0xFFFFFFFFu : 0u;
+    xm[j] = rel0 + 4 * j == 0 ? kInitRegister : 0u;
+  }
+  const uint32_t ntail = u.length & 3u;
+
+  auto packet_addr = [&](uint64_t r) -> uint64_t {
+    uint64_t p = first + r * P + c.grp;
+    p = p < u.count ? p : u.count - 1;
+    return u.base + p * u.stride;
+  };
+
+  uint64_t pa = packet_addr(0) + off0;
+  u32x4 q[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    q[s] = load_chunk(pa + (uint64_t)kBytesPerStep * s);
+    issue_order_fence();
+  }
+  uint32_t tw = 0;
+  if constexpr (kTail) tw = load_word(pa - off0 + g.a1);
+
+  for (uint64_t r = 0; r < nrounds; ++r) {
+    const uint64_t pn = packet_addr(r + 1) + off0;
+    uint32_t h0, h1, h2, h3;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const u32x4 w = q[s];
+      if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
+        h0 = (w.x & am[0]) ^ xm[0];
+        h1 = (w.y & am[1]) ^ xm[1];
+        h2 = (w.z & am[2]) ^ xm[2];
+        h3 = (w.w & am[3]) ^ xm[3];
+      } else {
+        h0 = horner_main(lds, h0, w.x, c.lp0, c.lp1);
+        h1 = horner_main(lds, h1, w.y, c.lp0, c.lp1);
+        h2 = horner_main(lds, h2, w.z, c.lp0, c.lp1);
+        h3 = horner_main(lds, h3, w.w, c.lp0, c.lp1);
+      }
+      issue_order_fence();
+      q[s] = load_chunk(pn + (uint64_t)kBytesPerStep * s);
+      issue_order_fence();
+    }
+    uint32_t tw_next = 0;
+    if constexpr (kTail) tw_next = load_word(pn - off0 + g.a1);
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
+    const uint64_t p = first + r * P + c.grp;
+    if (c.k == 0 && p < u.count) out[p] = __builtin_bswap32(~reg);
+    tw = tw_next;
+  }
+}
+
 }  // namespace
 
 int cu_count_for_current_device();
@@ -478,15 +581,57 @@ static unsigned grid_for(uint64_t count, hipError_t& err) {
   return (unsigned)blocks;
 }
 
+template <int NS, bool kTail>
+static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
+  hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  return hipGetLastError();
+}
+
+template <int... I>
+static hipError_t dispatch_uniform(int ns, bool tail, const UniformBatch& u, uint32_t* out, hipStream_t stream,
+                                   unsigned blocks, std::integer_sequence<int, I...>) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((ns == I + 1 ? (e = tail ? launch_uniform_ns<I + 1, true>(u, out, stream, blocks)
+                            : launch_uniform_ns<I + 1, false>(u, out, stream, blocks),
+                   true)
+                : false) ||
+   ...);
+  return e;
+}
+
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
                           uint32_t* out, hipStream_t stream) {
   if (count == 0) return hipSuccess;
   hipError_t err;
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  const int ns = make_geo(0, length).nsteps;
+  if (((b0 | stride) & 3u) == 0 && ns >= 1 && ns <= kMaxRoundSteps) {
+    // Packets whose top chunk would begin before `base` (only the first few) go
+    // through the streaming kernel; the rest through the uniform kernel.
+    const int64_t off_min = (int64_t)(length & ~3u) - 16 * kLanesPerPacket - (int64_t)kBytesPerStep * (ns - 1);
+    uint64_t p_min = 0;
+    if (off_min < 0) p_min = stride == 0 ? count : ((uint64_t)(-off_min) + stride - 1) / stride;
+    if (p_min > count) p_min = count;
+    if (p_min > 0) {
+      const unsigned blocks = grid_for(p_min, err);
+      if (err != hipSuccess) return err;
+      Launcher<false> L{Batch<false>{b0, nullptr, nullptr, stride, length, p_min}, out, stream, blocks};
+      err = L.streaming();
+      if (err != hipSuccess) return err;
+    }
+    if (p_min < count) {
+      const unsigned blocks = grid_for(count - p_min, err);
+      if (err != hipSuccess) return err;
+      const UniformBatch u{b0 + p_min * stride, stride, length, count - p_min};
+      return dispatch_uniform(ns, (length & 3u) != 0, u, out + p_min, stream, blocks,
+                              std::make_integer_sequence<int, kMaxRoundSteps>{});
+    }
+    return hipSuccess;
+  }
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
   // Packet starts cycle through phases (base + p*stride) mod 4: steps per packet.
   int hi = 0;
-  const uint64_t b0 = (uint64_t)(uintptr_t)base;
   for (uint64_t p = 0; p < 4 && p < count; ++p) {
     const int n = make_geo((b0 + p * stride) & 3u, length).nsteps;
     hi = n > hi ? n : hi;
