@@ -32,14 +32,20 @@
 //   crc32_stream_kernel<U>: any lengths.  A round is padded to a multiple of U
 //     slots and streamed through a U-deep ring; only round boundaries drain.
 //
-// LDS (one 1024-thread workgroup per CU, 144 KiB):
-//   [0, 128 KiB)  M32^32 tables replicated 32x: lane l always reads bank l%32,
-//                 conflict-free ds_read_b32.  Table t, entry i, bank b at dword
-//                 (t>>1)*16384 + i*64 + (t&1)*32 + b; the byte address is ONE
-//                 v_perm_b32 (byte1 = register byte t, byte0 = lane*4, byte2 = pair).
-//   [128 KiB, +)  unreplicated: M32^1 (set 0), tree operators M32^4/8/16 (sets 1..3).
+// LDS tables (80 KiB):
+//   [0, 64 KiB)   M32^32 tables t = 0..3 (one per register byte), 16 copies each:
+//                 entry i of copy c of table t at dword i*64 + t*16 + c, i.e. bank
+//                 (t&1)*16 + c.  ds_read_b32 serves lanes {0-31} and {32-63} in one
+//                 cycle each when no two lanes of a group hit one bank with different
+//                 addresses; lane l uses copy l%16, and in lookup j the lanes of the
+//                 lower 16 read table j while the upper 16 read table j^1: banks 0-15
+//                 vs 16-31, conflict-free.  Each address is ONE v_perm_b32 with a
+//                 per-lane selector (byte1 = register byte j^half, byte0 = copy/table).
+//   [64 KiB, +)   unreplicated: M32^1 (set 0), tree operators M32^4/8/16 (sets 1..3).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include <utility>
 
@@ -69,7 +75,8 @@ typedef __attribute__((address_space(1))) const U32x4A4 GlobalU32x4A4;
 constexpr int kBlock = 1024;
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int G = kLanesPerPacket;
-constexpr uint32_t kMainDwords = 32768;  // 4 tables x 256 entries x 32 banks
+constexpr uint32_t kMainCopies = 16;
+constexpr uint32_t kMainDwords = 4 * 256 * kMainCopies;  // 4 tables x 256 entries x 16 copies (64 KiB)
 
 constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 constexpr int kMainLevel = ilog2(4 * G);  // M32^(4G) = M32^32
@@ -89,14 +96,33 @@ __device__ __forceinline__ uint32_t lds_at(const uint32_t* lds, uint32_t byte_ad
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
 }
 
-// h' = M32^32(h) ^ w through the replicated tables.  lp0 = lane*4, lp1 = lane*4 | 64 KiB.
-__device__ __forceinline__ uint32_t horner_main(const uint32_t* lds, uint32_t h, uint32_t w, uint32_t lp0,
-                                                uint32_t lp1) {
-  const uint32_t a0 = __builtin_amdgcn_perm(h, lp0, 0x0C020400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(h, lp0, 0x0C020500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(h, lp1, 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(h, lp1, 0x0C020700u);
-  return xor3(xor3(lds_at(lds, a0), lds_at(lds, a1 + 128u), lds_at(lds, a2)), lds_at(lds, a3 + 128u), w);
+// Per-lane constants of the main-table lookups (see the LDS layout above).
+struct Lookup {
+  uint32_t lp;      // byte j: byte offset of this lane's copy of table t = j ^ half
+  uint32_t sel[4];  // v_perm selectors: byte0 <- lp byte j, byte1 <- h byte (j ^ half)
+};
+
+__device__ __forceinline__ Lookup make_lookup(uint32_t lane) {
+  const uint32_t half = (lane >> 4) & 1u, copy = lane & 15u;
+  Lookup lk;
+  lk.lp = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t t = j ^ half;
+    lk.lp |= (copy * 4u + 64u * t) << (8u * j);
+    lk.sel[j] = 0x0C0C0000u | ((4u + t) << 8) | j;
+  }
+  return lk;
+}
+
+// h' = M32^32(h) ^ w through the replicated tables: 4 v_perm (each one byte address)
+// + 4 conflict-free ds_read_b32.
+__device__ __forceinline__ uint32_t horner_main(const uint32_t* lds, uint32_t h, uint32_t w, const Lookup& lk) {
+  const uint32_t a0 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[0]);
+  const uint32_t a1 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[1]);
+  const uint32_t a2 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[2]);
+  const uint32_t a3 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[3]);
+  return xor3(xor3(lds_at(lds, a0), lds_at(lds, a1), lds_at(lds, a2)), lds_at(lds, a3), w);
 }
 
 // M32^n(x) through an unreplicated 4x256 table set.
@@ -129,9 +155,9 @@ __device__ __forceinline__ void fill_lds(uint32_t* lds) {
     const int tab = t >> 8, i = t & 255;
     const uint32_t v = g_op_tables.op[kMainLevel][tab][i];
     const u32x4 vv = {v, v, v, v};
-    u32x4* dst = reinterpret_cast<u32x4*>(lds + (tab >> 1) * 16384 + i * 64 + (tab & 1) * 32);
+    u32x4* dst = reinterpret_cast<u32x4*>(lds + i * 64 + tab * 16);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dst[j] = vv;
+    for (int j = 0; j < 4; ++j) dst[j] = vv;
   }
   for (int x = t; x < kSmallSets * 1024; x += kBlock) {
     const int set = x >> 10, rem = x & 1023;
@@ -264,7 +290,8 @@ __device__ __forceinline__ void finish_round(const uint32_t* lds, uint32_t h0, u
 __device__ __forceinline__ void issue_order_fence() { __builtin_amdgcn_sched_barrier(0); }
 
 struct LaneConsts {
-  uint32_t k, grp, lp0, lp1;
+  uint32_t k, grp;
+  Lookup lk;
   uint64_t base4, dummy;
 };
 
@@ -273,8 +300,7 @@ __device__ __forceinline__ LaneConsts lane_consts(uint64_t base) {
   const uint32_t lane = threadIdx.x & 63u;
   c.k = lane & (G - 1);
   c.grp = lane / G;
-  c.lp0 = (lane & 31u) << 2;
-  c.lp1 = c.lp0 | 0x10000u;
+  c.lk = make_lookup(lane);
   c.base4 = base & ~(uint64_t)3;
   c.dummy = (uint64_t)(uintptr_t)g_zero_chunk;
   return c;
@@ -361,10 +387,10 @@ __global__ __launch_bounds__(kBlock) void crc32_rounds_kernel(Batch<kRagged> b, 
       if (s == 0) {  // M32^32(0) = 0: the first step needs no lookups
         h0 = w0; h1 = w1; h2 = w2; h3 = w3;
       } else {
-        h0 = horner_main(lds, h0, w0, c.lp0, c.lp1);
-        h1 = horner_main(lds, h1, w1, c.lp0, c.lp1);
-        h2 = horner_main(lds, h2, w2, c.lp0, c.lp1);
-        h3 = horner_main(lds, h3, w3, c.lp0, c.lp1);
+        h0 = horner_main(lds, h0, w0, c.lk);
+        h1 = horner_main(lds, h1, w1, c.lk);
+        h2 = horner_main(lds, h2, w2, c.lk);
+        h3 = horner_main(lds, h3, w3, c.lk);
       }
       q[s] = load_chunk(slot_addr(nxt, s, c.dummy));
       issue_order_fence();
@@ -433,10 +459,10 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
           }
           if (top && (meta & kMetaHeadMask)) mask_top(meta, w0, w1, w2, w3);
         }
-        h0 = horner_main(lds, h0, w0, c.lp0, c.lp1);
-        h1 = horner_main(lds, h1, w1, c.lp0, c.lp1);
-        h2 = horner_main(lds, h2, w2, c.lp0, c.lp1);
-        h3 = horner_main(lds, h3, w3, c.lp0, c.lp1);
+        h0 = horner_main(lds, h0, w0, c.lk);
+        h1 = horner_main(lds, h1, w1, c.lk);
+        h2 = horner_main(lds, h2, w2, c.lk);
+        h3 = horner_main(lds, h3, w3, c.lk);
         q[s] = load_chunk(j + U < nslots ? addr_of(j + U) : c.dummy);
         issue_order_fence();
       }
@@ -517,10 +543,10 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, u
         h2 = (w.z & am[2]) ^ xm[2];
         h3 = (w.w & am[3]) ^ xm[3];
       } else {
-        h0 = horner_main(lds, h0, w.x, c.lp0, c.lp1);
-        h1 = horner_main(lds, h1, w.y, c.lp0, c.lp1);
-        h2 = horner_main(lds, h2, w.z, c.lp0, c.lp1);
-        h3 = horner_main(lds, h3, w.w, c.lp0, c.lp1);
+        h0 = horner_main(lds, h0, w.x, c.lk);
+        h1 = horner_main(lds, h1, w.y, c.lk);
+        h2 = horner_main(lds, h2, w.z, c.lk);
+        h3 = horner_main(lds, h3, w.w, c.lk);
       }
       issue_order_fence();
       q[s] = load_chunk(pn + (uint64_t)kBytesPerStep * s);
@@ -534,6 +560,175 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, u
     if (c.k == 0 && p < u.count) out[p] = __builtin_bswap32(~reg);
     tw = tw_next;
   }
+}
+
+// ---------------------------------------------------------------------------------
+// Uniform kernel, LDS-DMA form.  Same arithmetic as crc32_uniform_kernel, but each
+// slot's 1 KiB (64 lanes x 16 B) arrives through global_load_lds_dwordx4 into a
+// per-wave ring of kDmaRing LDS slots instead of VGPRs:
+//     wait for slot t -> ds_read_b128 -> DMA for slot t + kDmaRing into the same
+//     LDS slot -> table lookups for slot t.
+// kDmaRing KiB per wave, 16 waves: up to 80 KiB of reads in flight per CU, and the
+// returning data never competes with the lookups for VGPR write ports (register
+// rings lose bandwidth as per-slot VALU work grows).
+//
+// Waits.  hipcc drains vmcnt(0) before any LDS read it sees after an LDS-DMA, so the
+// ring read is one asm statement: s_waitcnt vmcnt(kDmaRing-1) (every DMA completes in
+// issue order and kDmaRing-1 DMAs are always issued after the one awaited; other
+// vector-memory ops only make the wait stricter), ds_read_b128, lgkmcnt(0) (the read
+// must retire before the slot is refilled).  The DMAs themselves are unconditional
+// (lanes past the end re-read the batch's last packet), so the count never drifts.
+//
+// Results of 8 rounds are collected in one register (lane 8g+j = round j's packet of
+// group g) and written by one store.  The whole batch goes through this kernel:
+// slot-0 chunks that lie wholly before their packet read the zero chunk; the one lane
+// whose slot-0 chunk straddles the packet start reads the straddled words with
+// load_top_words only when the chunk would reach below the caller's base.
+// ---------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void LdsVoid;
+constexpr int kDmaRing = 5;                                  // LDS slots per wave
+constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
+
+template <int N>
+__device__ __forceinline__ u32x4 read_landed_slot(uint32_t lds_addr) {
+  u32x4 v;
+  asm volatile(
+      "s_waitcnt vmcnt(%1)\n\t"
+      "ds_read_b128 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(v)
+      : "i"(N), "v"(lds_addr)
+      : "memory");
+  return v;
+}
+
+// The 8 groups' trailing-byte words, via the scalar unit (a vector load here would
+// make hipcc drain the DMA ring to wait for it).  Lane of group g gets word g.
+__device__ __forceinline__ uint32_t tail_words_scalar(const uint64_t (&a)[8], uint32_t grp) {
+  uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+  asm volatile(
+      "s_load_dword %0, %8, 0x0\n\t"
+      "s_load_dword %1, %9, 0x0\n\t"
+      "s_load_dword %2, %10, 0x0\n\t"
+      "s_load_dword %3, %11, 0x0\n\t"
+      "s_load_dword %4, %12, 0x0\n\t"
+      "s_load_dword %5, %13, 0x0\n\t"
+      "s_load_dword %6, %14, 0x0\n\t"
+      "s_load_dword %7, %15, 0x0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(t0), "=&s"(t1), "=&s"(t2), "=&s"(t3), "=&s"(t4), "=&s"(t5), "=&s"(t6), "=&s"(t7)
+      : "s"(a[0]), "s"(a[1]), "s"(a[2]), "s"(a[3]), "s"(a[4]), "s"(a[5]), "s"(a[6]), "s"(a[7])
+      : "memory");
+  uint32_t w = t0;
+  w = grp == 1 ? t1 : w;
+  w = grp == 2 ? t2 : w;
+  w = grp == 3 ? t3 : w;
+  w = grp == 4 ? t4 : w;
+  w = grp == 5 ? t5 : w;
+  w = grp == 6 ? t6 : w;
+  w = grp == 7 ? t7 : w;
+  return w;
+}
+
+template <int NS, bool kTail>
+__global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
+  __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(u.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wv);
+  const uint64_t first = (uint64_t)wave * kPacketsPerWave;
+  const uint64_t P = (uint64_t)gridDim.x * kWavesPerBlock * kPacketsPerWave;
+  if (first >= u.count) return;
+  const uint64_t nrounds = (u.count - first + P - 1) / P;
+
+  const PacketGeo g = make_geo(0, u.length);
+  // This lane's slot-0 chunk relative to its packet's start (> -128: DESIGN.md §3).
+  const int64_t rel0 = (int64_t)g.a1 - 16 * (int64_t)(c.k + 1u) - (int64_t)kBytesPerStep * (NS - 1);
+  uint32_t am[4], xm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    am[j] = rel0 + 4 * j >= 0 ? 0xFFFFFFFFu : 0u;
+    xm[j] = rel0 + 4 * j == 0 ? kInitRegister : 0u;
+  }
+  const bool none0 = rel0 <= -16;             // slot-0 chunk wholly before the packet
+  const bool part0 = rel0 < 0 && rel0 > -16;  // straddles the packet start
+  const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;  // round_meta()'s head field
+  const uint32_t ntail = u.length & 3u;
+
+  auto packet_index = [&](uint64_t r, uint32_t grp) -> uint64_t {
+    const uint64_t p = first + r * P + grp;
+    return p < u.count ? p : u.count - 1;  // lanes past the end re-read the last packet, never store
+  };
+  auto packet_base = [&](uint64_t r) -> uint64_t { return u.base + packet_index(r, c.grp) * u.stride; };
+  auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
+  auto slot_src = [&](uint64_t pb, int s) -> uint64_t {
+    if (s != 0) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * s);
+    return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
+  };
+  // LDS byte address of ring position 0 for this wave; DMA destinations are wave-uniform.
+  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
+  auto dma = [&](uint64_t src, uint32_t q) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 0);
+  };
+
+#pragma unroll
+  for (int f = 0; f < kDmaRing; ++f) dma(slot_src(packet_base(f / NS), f % NS), (uint32_t)f);
+  uint32_t q = 0;  // ring position of the next slot to consume (wave-uniform)
+  uint32_t res = 0;
+  for (uint64_t r = 0; r < nrounds; ++r) {
+    const uint64_t pb = packet_base(r);
+    uint32_t tw = 0;
+    if constexpr (kTail) {
+      uint64_t ta[8];
+#pragma unroll
+      for (uint32_t gi = 0; gi < 8; ++gi) ta[gi] = u.base + packet_index(r, gi) * u.stride + g.a1;
+      tw = tail_words_scalar(ta, c.grp);
+    }
+    uint32_t h0, h1, h2, h3;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
+      {
+        const int f = s + kDmaRing;  // slot f % NS of round r + f / NS
+        dma(slot_src(packet_base(r + (uint64_t)(f / NS)), f % NS), q);
+      }
+      q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
+      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+      if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
+        const bool below = is_below(pb);
+        if (__builtin_amdgcn_ballot_w64(below)) {
+          if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
+        }
+        h0 = (w0 & am[0]) ^ xm[0];
+        h1 = (w1 & am[1]) ^ xm[1];
+        h2 = (w2 & am[2]) ^ xm[2];
+        h3 = (w3 & am[3]) ^ xm[3];
+      } else {
+        h0 = horner_main(lds, h0, w0, c.lk);
+        h1 = horner_main(lds, h1, w1, c.lk);
+        h2 = horner_main(lds, h2, w2, c.lk);
+        h3 = horner_main(lds, h3, w3, c.lk);
+      }
+      issue_order_fence();  // keep each slot's lookups between its DMA and the next slot's wait
+    }
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
+    // Lane 8g+j keeps round (r & ~7) + j's checksum of group g.
+    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    const uint32_t j = (uint32_t)(r & 7u);
+    if (c.k == j) res = crc;
+    if (j == 7u || r + 1 == nrounds) {
+      const uint64_t p = first + (r - j + c.k) * P + c.grp;
+      if (c.k <= j && p < u.count) out[p] = res;
+    }
+  }
+  // The ring's last DMAs (re-reads of valid packets) must land before the wave's LDS goes away.
+  __builtin_amdgcn_s_waitcnt(0);
 }
 
 }  // namespace
@@ -582,21 +777,34 @@ static unsigned grid_for(uint64_t count, hipError_t& err) {
 }
 
 template <int NS, bool kTail>
-static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
-  hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks,
+                                   bool dma) {
+  if (dma)
+    hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  else
+    hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
 
 template <int... I>
 static hipError_t dispatch_uniform(int ns, bool tail, const UniformBatch& u, uint32_t* out, hipStream_t stream,
-                                   unsigned blocks, std::integer_sequence<int, I...>) {
+                                   unsigned blocks, bool dma, std::integer_sequence<int, I...>) {
   hipError_t e = hipErrorInvalidValue;
-  (void)((ns == I + 1 ? (e = tail ? launch_uniform_ns<I + 1, true>(u, out, stream, blocks)
-                            : launch_uniform_ns<I + 1, false>(u, out, stream, blocks),
+  (void)((ns == I + 1 ? (e = tail ? launch_uniform_ns<I + 1, true>(u, out, stream, blocks, dma)
+                            : launch_uniform_ns<I + 1, false>(u, out, stream, blocks, dma),
                    true)
                 : false) ||
    ...);
   return e;
+}
+
+// ENET_CRC_UNIFORM=regs selects the register-ring uniform kernel (kept for A/B runs).
+static bool use_dma_uniform() {
+  static const bool dma = [] {
+    const char* v = getenv("ENET_CRC_UNIFORM");
+    return !(v && strcmp(v, "regs") == 0);
+  }();
+  return dma;
 }
 
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
@@ -606,8 +814,15 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
   const int ns = make_geo(0, length).nsteps;
   if (((b0 | stride) & 3u) == 0 && ns >= 1 && ns <= kMaxRoundSteps) {
-    // Packets whose top chunk would begin before `base` (only the first few) go
-    // through the streaming kernel; the rest through the uniform kernel.
+    const bool tail = (length & 3u) != 0;
+    if (use_dma_uniform()) {  // one launch covers the whole batch
+      const unsigned blocks = grid_for(count, err);
+      if (err != hipSuccess) return err;
+      return dispatch_uniform(ns, tail, UniformBatch{b0, stride, length, count}, out, stream, blocks, true,
+                              std::make_integer_sequence<int, kMaxRoundSteps>{});
+    }
+    // Register-ring kernel: packets whose top chunk would begin before `base` (only
+    // the first few) go through the streaming kernel, the rest through the uniform one.
     const int64_t off_min = (int64_t)(length & ~3u) - 16 * kLanesPerPacket - (int64_t)kBytesPerStep * (ns - 1);
     uint64_t p_min = 0;
     if (off_min < 0) p_min = stride == 0 ? count : ((uint64_t)(-off_min) + stride - 1) / stride;
@@ -623,7 +838,7 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
       const unsigned blocks = grid_for(count - p_min, err);
       if (err != hipSuccess) return err;
       const UniformBatch u{b0 + p_min * stride, stride, length, count - p_min};
-      return dispatch_uniform(ns, (length & 3u) != 0, u, out + p_min, stream, blocks,
+      return dispatch_uniform(ns, tail, u, out + p_min, stream, blocks, false,
                               std::make_integer_sequence<int, kMaxRoundSteps>{});
     }
     return hipSuccess;

@@ -1,8 +1,10 @@
 #!/usr/bin/env bash
-# Time every tools/ablate/bin/* variant, then read its effective clock with rocprofv3.
+# Time every tools/ablate/bin/* variant (DMA and register-ring uniform kernels), then
+# read each one's effective clock with rocprofv3 (GRBM_GUI_ACTIVE / duration).
 set -u
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 for b in "$R"/tools/ablate/bin/*; do timeout -k 5 60 "$b" || exit 1; done
+for b in "$R"/tools/ablate/bin/*; do ENET_CRC_UNIFORM=regs timeout -k 5 60 "$b" | sed 's/^/regs:/' || exit 1; done
 cd /tmp && export TMPDIR=/tmp
 for b in "$R"/tools/ablate/bin/*; do
   n=$(basename "$b")
