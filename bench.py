@@ -3,11 +3,14 @@
 
     python bench.py [--gpus N --steps K --warmup W --config uniform|ragged|large]
 
-One step = one launch of the batch kernel over this rank's whole shard
-(default: 1M x 1200-byte packets = BASELINE configs[1]), inputs already resident
-in HBM.  N > 1 runs one process per GPU (torch.distributed.run); shards are
-independent (no data-path collective), so per-GPU work is fixed: weak scaling.
-Rank 0 prints one JSON line.
+One step = one launch of the batch kernel over this rank's whole shard, inputs
+already resident in HBM.  Default workload: 1M x 1200-byte packets on 1 GPU
+(BASELINE configs[1]); with N > 1 GPUs each rank takes 2M packets, so N = 8 is
+configs[3] (16M x 1200 B sharded 8 ways).  One process per GPU
+(torch.distributed.run); shards are independent (no data-path collective), per-GPU
+work is fixed as N grows: weak scaling.  Rank 0 prints one JSON line, which at
+N = 1 also carries the CPU baseline (oracle on the host cores) and the
+end-to-end host->device->host rate of the host-memory entry point.
 """
 from __future__ import annotations
 
@@ -25,23 +28,31 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 import rusty_enet_amd as rea  # noqa: E402
+from rusty_enet_amd.shards import max_over_ranks  # noqa: E402
 from _data import ENET_SEED, packed_offsets, ragged_lengths  # noqa: E402
 
 METRIC = "device-resident GiB/s, batched CRC-32 over ENet packets; % HBM3E peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 CONFIGS = {
-    # name: (description, packets per GPU)
-    "uniform": ("1M x 1200-byte packets per GPU (ENet batch, uniform stride 1200)", 1 << 20),
-    "ragged": ("1M packets per GPU, lengths U{64..1392}, packed at byte offsets", 1 << 20),
-    "large": ("32768 x 64 KiB buffers per GPU (large-buffer path)", 32768),
+    # name: (description, packets per GPU at N = 1, packets per GPU at N > 1)
+    "uniform": ("1200-byte packets, uniform stride 1200 (ENet batch); BASELINE configs[1] / configs[3]",
+                1 << 20, 2 << 20),
+    "ragged": ("ragged packets, lengths U{64..1392}, packed at byte offsets; BASELINE configs[2]",
+               1 << 20, 1 << 20),
+    "large": ("64 KiB buffers, one CRC each (large-buffer path); BASELINE configs[4]", 32768, 32768),
 }
 
 
-def make_workload(name: str, rank: int, dev):
+def packets_per_gpu(name: str, world: int) -> int:
+    _, n1, nn = CONFIGS[name]
+    return n1 if world == 1 else nn
+
+
+def make_workload(name: str, rank: int, world: int, dev):
     g = torch.Generator(device=dev)
     g.manual_seed(ENET_SEED + 7919 * rank)
-    _, n = CONFIGS[name]
+    n = packets_per_gpu(name, world)
     if name == "uniform":
         L = 1200
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
@@ -114,6 +125,42 @@ def cpu_baseline(seconds: float = 10.0) -> dict:
             "all_cores": {"value": round(multi, 4), "cores": threads}}
 
 
+def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
+    """Host buffers -> pinned staging -> H2D -> kernel -> D2H (enet_crc32_ragged_host),
+    plus the per-call latency of the drop-in hook (enet_crc32_iov, one datagram)."""
+    import _oracle
+    from _data import splitmix64_bytes
+
+    data = splitmix64_bytes(ENET_SEED + 99, n * L)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    ln = np.full(n, L, dtype=np.uint32)
+    ctx = rea.Context(dev.index or 0)
+    got = ctx.crc32_ragged_host(data, off, ln)  # warm-up (grows the staging)
+    m = 4096
+    want = _oracle.crc32_uniform(data[: m * L], L, L, m)
+    if not np.array_equal(got[:m], want):
+        raise SystemExit("bench: end-to-end checksums differ from the oracle")
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        ctx.crc32_ragged_host(data, off, ln)
+        times.append(time.perf_counter() - t0)
+    rate = n * L / float(np.median(times)) / 2**30
+    pkt = [data[:1392]]
+    for _ in range(50):
+        ctx.crc32(pkt)
+    t0 = time.perf_counter()
+    calls = 2000
+    for _ in range(calls):
+        ctx.crc32(pkt)
+    per_call_us = (time.perf_counter() - t0) / calls * 1e6
+    ctx.close()
+    return {"value": round(rate, 3), "unit": "GiB/s", "path": "enet_crc32_ragged_host",
+            "sample": f"{n} x {L} B from pageable host memory, median of 5 passes",
+            "per_call_us": round(per_call_us, 2),
+            "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000"}
+
+
 def load_pmc_traffic(config: str):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
@@ -132,6 +179,7 @@ def main() -> None:
     ap.add_argument("--config", choices=sorted(CONFIGS), default="uniform")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host-memory measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,7 +193,7 @@ def main() -> None:
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    step, nbytes, npk, out, spec = make_workload(args.config, rank, dev)
+    step, nbytes, npk, out, spec = make_workload(args.config, rank, world, dev)
     step()
     torch.cuda.synchronize()
     if not args.no_verify:
@@ -170,10 +218,7 @@ def main() -> None:
     barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # average launch duration on that stream
-    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    wall_max, kernel_ms_max = float(t[0]), float(t[1])
+    wall_max, kernel_ms_max = max_over_ranks([wall, kernel_ms], device=dev)
     ms_per_step = wall_max * 1000.0 / args.steps
 
     if rank == 0:
@@ -186,7 +231,8 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (torch.randint bytes on device, seeded)",
-            "config": {"workload": CONFIGS[args.config][0], "packets_per_gpu": npk, "bytes_per_gpu": nbytes,
+            "config": {"workload": f"{npk} x " + CONFIGS[args.config][0] + " per GPU", "packets_per_gpu": npk,
+                       "bytes_per_gpu": nbytes,
                        "parallelism": f"{world} independent shards, no collective"},
             "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -195,6 +241,8 @@ def main() -> None:
         }
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if world == 1 and not args.no_e2e:
+            line["end_to_end"] = end_to_end(dev)
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -32,7 +32,7 @@ echo "[gpu_check] rocprofv3 kernel trace" >&2
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${CFG}_$TAG" -o run --output-format csv \
-  -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 5 --cpu-seconds 0 --no-verify \
+  -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 5 --cpu-seconds 0 --no-verify --no-e2e \
   > "$OUT/prof_${CFG}_$TAG.log" 2>&1
 prc=$?
 echo "[gpu_check] rocprof rc=$prc" >&2

@@ -16,7 +16,7 @@ for counters in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLE
                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $counters -d "$OUT/pass$i" -o run --output-format csv \
-    -- python3 "$ROOT/bench.py" --config "$CFG" --steps 5 --warmup 1 --cpu-seconds 0 --no-verify "$@" \
+    -- python3 "$ROOT/bench.py" --config "$CFG" --steps 5 --warmup 1 --cpu-seconds 0 --no-verify --no-e2e "$@" \
     > "$OUT/pass$i.log" 2>&1
   rc=$?
   echo "[pmc] pass $i ($counters) rc=$rc" >&2
