@@ -258,10 +258,18 @@ __device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_
   uint32_t y = apply_small(m1, h0) ^ h1;
   y = apply_small(m1, y) ^ h2;
   y = apply_small(m1, y) ^ h3;
-  y ^= from_lane_plus<1>(apply_small(lds + kMainDwords + 1024, y));
-  y ^= from_lane_plus<2>(apply_small(lds + kMainDwords + 2048, y));
-  y ^= from_lane_plus<4>(apply_small(lds + kMainDwords + 3072, y));
-  return apply_small(m1, y);
+  // Tree levels: only the lanes whose value moves down look it up (the others are
+  // masked off, which also keeps them out of the unreplicated tables' bank conflicts).
+  const uint32_t k = threadIdx.x & (G - 1);
+  uint32_t t = 0;
+  if (k & 1u) t = apply_small(lds + kMainDwords + 1024, y);
+  y ^= from_lane_plus<1>(t);
+  if ((k & 3u) == 2u) t = apply_small(lds + kMainDwords + 2048, y);
+  y ^= from_lane_plus<2>(t);
+  if (k == 4u) t = apply_small(lds + kMainDwords + 3072, y);
+  y ^= from_lane_plus<4>(t);
+  if (k == 0u) y = apply_small(m1, y);
+  return y;
 }
 
 // Sarwate byte steps (src/crc32.rs:43) over `ntail` bytes of `word` from byte `tsh`.
@@ -587,19 +595,32 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, u
 // ---------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void LdsVoid;
 constexpr int kDmaRing = 5;                                  // LDS slots per wave
+constexpr int kDmaRounds = 1;                                // rounds interleaved per wave
 constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
 
-template <int N>
-__device__ __forceinline__ u32x4 read_landed_slot(uint32_t lds_addr) {
-  u32x4 v;
-  asm volatile(
-      "s_waitcnt vmcnt(%1)\n\t"
-      "ds_read_b128 %0, %2\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=v"(v)
-      : "i"(N), "v"(lds_addr)
-      : "memory");
-  return v;
+// Wait until at most N DMAs are outstanding, read W landed slots (16 B per lane each),
+// and wait for the reads (the slots are refilled right after).
+template <int N, int W>
+__device__ __forceinline__ void read_landed_slots(const uint32_t (&addr)[W], u32x4 (&v)[W]) {
+  if constexpr (W == 1) {
+    asm volatile(
+        "s_waitcnt vmcnt(%1)\n\t"
+        "ds_read_b128 %0, %2\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(v[0])
+        : "i"(N), "v"(addr[0])
+        : "memory");
+  } else {
+    static_assert(W == 2, "1 or 2 interleaved rounds");
+    asm volatile(
+        "s_waitcnt vmcnt(%2)\n\t"
+        "ds_read_b128 %0, %3\n\t"
+        "ds_read_b128 %1, %4\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1])
+        : "i"(N), "v"(addr[0]), "v"(addr[1])
+        : "memory");
+  }
 }
 
 // The 8 groups' trailing-byte words, via the scalar unit (a vector load here would
@@ -630,10 +651,13 @@ __device__ __forceinline__ uint32_t tail_words_scalar(const uint64_t (&a)[8], ui
   return w;
 }
 
-template <int NS, bool kTail>
+// W rounds (8W packets) are processed together: W independent sets of 4 Horner
+// chains per lane, so each wait on the LDS lookups covers twice the work.
+template <int NS, bool kTail, int W>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
+  static_assert(kDmaRing > W, "ring must hold more than one step");
   fill_lds(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(u.base);
@@ -645,6 +669,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   const uint64_t P = (uint64_t)gridDim.x * kWavesPerBlock * kPacketsPerWave;
   if (first >= u.count) return;
   const uint64_t nrounds = (u.count - first + P - 1) / P;
+  const uint64_t nsuper = (nrounds + W - 1) / W;
 
   const PacketGeo g = make_geo(0, u.length);
   // This lane's slot-0 chunk relative to its packet's start (> -128: DESIGN.md §3).
@@ -660,11 +685,12 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;  // round_meta()'s head field
   const uint32_t ntail = u.length & 3u;
 
-  auto packet_index = [&](uint64_t r, uint32_t grp) -> uint64_t {
-    const uint64_t p = first + r * P + grp;
+  // Round rho of this wave: packets first + rho*P + (0..7).
+  auto packet_index = [&](uint64_t rho, uint32_t grp) -> uint64_t {
+    const uint64_t p = first + rho * P + grp;
     return p < u.count ? p : u.count - 1;  // lanes past the end re-read the last packet, never store
   };
-  auto packet_base = [&](uint64_t r) -> uint64_t { return u.base + packet_index(r, c.grp) * u.stride; };
+  auto packet_base = [&](uint64_t rho) -> uint64_t { return u.base + packet_index(rho, c.grp) * u.stride; };
   auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
   auto slot_src = [&](uint64_t pb, int s) -> uint64_t {
     if (s != 0) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * s);
@@ -675,56 +701,88 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   auto dma = [&](uint64_t src, uint32_t q) {
     __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 0);
   };
+  // DMA unit i of super-round r (i = s*W + w): slot s of round r*W + w.
+  constexpr int kUnits = NS * W;
+  auto unit_src = [&](uint64_t r, int i) -> uint64_t {
+    const uint64_t rr = r + (uint64_t)(i / kUnits);
+    const int rem = i % kUnits;
+    return slot_src(packet_base(rr * W + (uint64_t)(rem % W)), rem / W);
+  };
 
 #pragma unroll
-  for (int f = 0; f < kDmaRing; ++f) dma(slot_src(packet_base(f / NS), f % NS), (uint32_t)f);
-  uint32_t q = 0;  // ring position of the next slot to consume (wave-uniform)
+  for (int f = 0; f < kDmaRing; ++f) dma(unit_src(0, f), (uint32_t)f);
+  uint32_t q = 0;  // ring position of the next unit to consume (wave-uniform)
   uint32_t res = 0;
-  for (uint64_t r = 0; r < nrounds; ++r) {
-    const uint64_t pb = packet_base(r);
-    uint32_t tw = 0;
-    if constexpr (kTail) {
-      uint64_t ta[8];
+  for (uint64_t r = 0; r < nsuper; ++r) {
+    uint64_t pb[W];
+    uint32_t tw[W];
 #pragma unroll
-      for (uint32_t gi = 0; gi < 8; ++gi) ta[gi] = u.base + packet_index(r, gi) * u.stride + g.a1;
-      tw = tail_words_scalar(ta, c.grp);
+    for (int w = 0; w < W; ++w) {
+      pb[w] = packet_base(r * W + w);
+      tw[w] = 0;
+      if constexpr (kTail) {
+        uint64_t ta[8];
+#pragma unroll
+        for (uint32_t gi = 0; gi < 8; ++gi) ta[gi] = u.base + packet_index(r * W + w, gi) * u.stride + g.a1;
+        tw[w] = tail_words_scalar(ta, c.grp);
+      }
     }
-    uint32_t h0, h1, h2, h3;
+    uint32_t h[W][4];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
-      {
-        const int f = s + kDmaRing;  // slot f % NS of round r + f / NS
-        dma(slot_src(packet_base(r + (uint64_t)(f / NS)), f % NS), q);
+      uint32_t addr[W];
+      u32x4 v[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const uint32_t qw = q + w < (uint32_t)kDmaRing ? q + w : q + w - kDmaRing;
+        addr[w] = ring0 + qw * kRingStride + lane * 16u;
       }
-      q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
-      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-      if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
-        const bool below = is_below(pb);
-        if (__builtin_amdgcn_ballot_w64(below)) {
-          if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
+      read_landed_slots<kDmaRing - W, W>(addr, v);
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const uint32_t qw = q + w < (uint32_t)kDmaRing ? q + w : q + w - kDmaRing;
+        dma(unit_src(r, s * W + w + kDmaRing), qw);
+      }
+      q = q + W < (uint32_t)kDmaRing ? q + W : q + W - kDmaRing;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint32_t w0 = v[w].x, w1 = v[w].y, w2 = v[w].z, w3 = v[w].w;
+        if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
+          const bool below = is_below(pb[w]);
+          if (__builtin_amdgcn_ballot_w64(below)) {
+            if (below) load_top_words(pb[w] + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
+          }
+          h[w][0] = (w0 & am[0]) ^ xm[0];
+          h[w][1] = (w1 & am[1]) ^ xm[1];
+          h[w][2] = (w2 & am[2]) ^ xm[2];
+          h[w][3] = (w3 & am[3]) ^ xm[3];
+        } else {
+          h[w][0] = horner_main(lds, h[w][0], w0, c.lk);
+          h[w][1] = horner_main(lds, h[w][1], w1, c.lk);
+          h[w][2] = horner_main(lds, h[w][2], w2, c.lk);
+          h[w][3] = horner_main(lds, h[w][3], w3, c.lk);
         }
-        h0 = (w0 & am[0]) ^ xm[0];
-        h1 = (w1 & am[1]) ^ xm[1];
-        h2 = (w2 & am[2]) ^ xm[2];
-        h3 = (w3 & am[3]) ^ xm[3];
-      } else {
-        h0 = horner_main(lds, h0, w0, c.lk);
-        h1 = horner_main(lds, h1, w1, c.lk);
-        h2 = horner_main(lds, h2, w2, c.lk);
-        h3 = horner_main(lds, h3, w3, c.lk);
       }
-      issue_order_fence();  // keep each slot's lookups between its DMA and the next slot's wait
+      issue_order_fence();  // keep each step's lookups between its DMAs and the next step's wait
     }
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
-    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
-    // Lane 8g+j keeps round (r & ~7) + j's checksum of group g.
-    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
-    const uint32_t j = (uint32_t)(r & 7u);
-    if (c.k == j) res = crc;
-    if (j == 7u || r + 1 == nrounds) {
-      const uint64_t p = first + (r - j + c.k) * P + c.grp;
-      if (c.k <= j && p < u.count) out[p] = res;
+    uint32_t crc[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t reg = combine_streams(lds, h[w][0], h[w][1], h[w][2], h[w][3]);
+      if constexpr (kTail) reg = tail_steps(lds, reg, tw[w], ntail, 0);
+      crc[w] = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    }
+    // Lane 8g+j keeps round (rho & ~7) + j's checksum of group g; one store per 8 rounds.
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const uint64_t rho = r * W + w;
+      if (W > 1 && rho >= nrounds) break;
+      const uint32_t j = (uint32_t)(rho & 7u);
+      if (c.k == j) res = crc[w];
+      if (j == 7u || rho + 1 == nrounds) {
+        const uint64_t p = first + (rho - j + c.k) * P + c.grp;
+        if (c.k <= j && p < u.count) out[p] = res;
+      }
     }
   }
   // The ring's last DMAs (re-reads of valid packets) must land before the wave's LDS goes away.
@@ -780,7 +838,8 @@ template <int NS, bool kTail>
 static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks,
                                    bool dma) {
   if (dma)
-    hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+    hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS, kTail, kDmaRounds>), dim3(blocks), dim3(kBlock), 0, stream, u,
+                       out);
   else
     hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();

@@ -1,0 +1,118 @@
+// LDS-DMA streaming probe (tooling, not product): does the ACCESS PATTERN of the
+// CRC kernel's DMA ring limit its bandwidth?  Same ring as crc32_uniform_dma_kernel
+// (5 x 1 KiB per wave, 16 waves/CU, 80 KiB of other LDS), same asm waits.
+//   pattern 0: global streaming, wave's slot t = 1 KiB piece (t * nwaves + wave)
+//   pattern 1: CRC kernel shape, 8 packets x 128 B at packet offset 128 s - 80 (1200-B packets)
+//   pattern 2: CRC shape, 16-B aligned within the packet (offset 128 s)
+//   pattern 3: block-contiguous: round = 8 packets = 9600 B, slot s = bytes [1024 s, +1024)
+// work = 0: XOR only; work = 1: 16 table lookups per slot (the kernel's per-slot LDS load).
+//   hipcc --offload-arch=gfx950 -O3 -o tools/dma_probe tools/dma_probe.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void LdsVoid;
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+constexpr int R = 5, NS = 10;
+
+__device__ __forceinline__ u32x4 read_slot(uint32_t a) {
+  u32x4 v;
+  asm volatile("s_waitcnt vmcnt(4)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+
+template <int PAT, int WORK, int NT>
+__global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, uint64_t npk, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[20480];
+  __shared__ __attribute__((aligned(16))) u32x4 ring[R][16][64];
+  for (int i = threadIdx.x; i < 20480; i += 1024) tab[i] = i * 2654435761u;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = lane / 8, k = lane % 8;
+  const uint64_t wave = (uint64_t)blockIdx.x * 16 + wv, nwaves = (uint64_t)gridDim.x * 16;
+  const uint64_t nrounds_total = npk / 8;
+  const uint64_t nr = wave < nrounds_total ? (nrounds_total - wave + nwaves - 1) / nwaves : 0;
+  const uint64_t base = (uint64_t)(uintptr_t)buf;
+  auto src = [&](uint64_t r, int s) -> uint64_t {
+    const uint64_t rr = wave + (r < nr ? r : nr - 1) * nwaves;  // global round index
+    if (PAT == 0) return base + ((uint64_t)(rr * NS + s) % (npk * 1200 / 1024)) * 1024 + lane * 16;
+    if (PAT == 3) return base + rr * 9600 + (uint64_t)s * 1024 + lane * 16;
+    const uint64_t pb = base + (rr * 8 + g) * 1200;
+    int64_t off = (PAT == 1 ? -80 : 0) + 128 * s + 16 * (int)k;
+    if (off < 0 && rr * 8 + g == 0) off = 0;
+    if (off + 16 > 1200) off = 1200 - 16;
+    return pb + off;
+  };
+  auto dma = [&](uint64_t a, uint32_t q) {
+    __builtin_amdgcn_global_load_lds((const void*)a, (LdsVoid*)&ring[q][wv][0], 16, 0, NT ? 2 : 0);
+  };
+  if (nr == 0) return;
+  for (int f = 0; f < R; ++f) dma(src(f / NS, f % NS), f);
+  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
+  uint32_t q = 0, h0 = lane, h1 = lane * 3, h2 = lane * 5, h3 = lane * 7;
+  for (uint64_t r = 0; r < nr; ++r) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const u32x4 v = read_slot(ring0 + q * 16384u + lane * 16u);
+      const int f = s + R;
+      dma(src(r + f / NS, f % NS), q);
+      q = q + 1 == R ? 0 : q + 1;
+      if (WORK) {
+        auto step = [&](uint32_t h, uint32_t w) {
+          return tab[h & 0xff] ^ tab[256 + ((h >> 8) & 0xff)] ^ tab[512 + ((h >> 16) & 0xff)] ^ tab[768 + (h >> 24)] ^ w;
+        };
+        h0 = step(h0, v.x); h1 = step(h1, v.y); h2 = step(h2, v.z); h3 = step(h3, v.w);
+      } else {
+        h0 ^= v.x; h1 ^= v.y; h2 ^= v.z; h3 ^= v.w;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  out[blockIdx.x * 1024 + threadIdx.x] = h0 ^ h1 ^ h2 ^ h3;
+}
+
+template <int PAT, int WORK, int NT>
+static void run(const char* name, const uint8_t* d, uint64_t npk, uint32_t* out, int blocks) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
+  CHECK(hipDeviceSynchronize());
+  const int iters = 20;
+  CHECK(hipEventRecord(e0, 0));
+  for (int w = 0; w < iters; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
+  CHECK(hipEventRecord(e1, 0));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1000.0 / iters;
+  printf("%-44s %8.1f us  %7.1f GB/s\n", name, us, npk * 1200.0 / (us * 1e3));
+}
+
+int main() {
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const uint64_t npk = 1 << 20, bytes = npk * 1200 + 4096;
+  uint8_t* d;
+  uint32_t* out;
+  CHECK(hipMalloc(&d, bytes));
+  CHECK(hipMalloc(&out, 64 << 20));
+  CHECK(hipMemset(d, 0x5a, bytes));
+  printf("CUs=%d, 1M x 1200 B\n", cus);
+  run<0, 0, 0>("P0 global stream, xor", d, npk, out, cus);
+  run<1, 0, 0>("P1 crc shape (-80), xor", d, npk, out, cus);
+  run<2, 0, 0>("P2 crc shape aligned, xor", d, npk, out, cus);
+  run<3, 0, 0>("P3 block-contiguous, xor", d, npk, out, cus);
+  run<0, 1, 0>("P0 global stream, lookups", d, npk, out, cus);
+  run<1, 1, 0>("P1 crc shape (-80), lookups", d, npk, out, cus);
+  run<2, 1, 0>("P2 crc shape aligned, lookups", d, npk, out, cus);
+  run<3, 1, 0>("P3 block-contiguous, lookups", d, npk, out, cus);
+  run<1, 0, 1>("P1 crc shape (-80), xor, nt", d, npk, out, cus);
+  run<3, 0, 1>("P3 block-contiguous, xor, nt", d, npk, out, cus);
+  run<1, 1, 1>("P1 crc shape (-80), lookups, nt", d, npk, out, cus);
+  return 0;
+}
