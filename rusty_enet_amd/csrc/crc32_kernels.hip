@@ -174,13 +174,25 @@ struct Batch {
   uint64_t stride;
   uint32_t length;
   uint64_t count;
+  const uint32_t* perm = nullptr;  // ragged: optional processing order (packet ids sorted by step count)
 };
 
-// Descriptor of packet p (p >= count reads as an empty packet at offset 0).
+// Packet id processed in position p (the identity unless the batch is permuted).
+template <bool kRagged>
+__device__ __forceinline__ uint64_t packet_id(const Batch<kRagged>& b, uint64_t p) {
+  if constexpr (kRagged) {
+    const uint64_t q = p < b.count ? p : b.count - 1;
+    return b.perm ? (uint64_t)b.perm[q] : q;
+  } else {
+    return p;
+  }
+}
+
+// Descriptor of the packet in position p (p >= count reads as an empty packet).
 template <bool kRagged>
 __device__ __forceinline__ void load_desc(const Batch<kRagged>& b, uint64_t p, uint64_t& off, uint32_t& len) {
   if constexpr (kRagged) {
-    const uint64_t q = p < b.count ? p : b.count - 1;
+    const uint64_t q = packet_id(b, p);
     off = b.offsets[q];
     len = p < b.count ? b.lengths[q] : 0;
   } else {
@@ -475,8 +487,75 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
         issue_order_fence();
       }
     }
-    finish_round(lds, h0, h1, h2, h3, meta, tail_word, c.k, out + p);
+    finish_round(lds, h0, h1, h2, h3, meta, tail_word, c.k, out + packet_id(b, p));
   }
+}
+
+// ---------------------------------------------------------------------------------
+// Ragged batches: order the packets by step count first (a counting sort on device),
+// so the 8 packets of a streaming-kernel round need the same number of slots instead
+// of all being padded to the longest.  Three small kernels, O(12 B) per packet:
+//   hist:    per-workgroup histogram of step classes over a contiguous packet range,
+//            stored class-major (hist[class * G + block]);
+//   scan:    exclusive scan of that array in place (one workgroup): entry
+//            (class, block) becomes the first output position of that block's packets
+//            of that class;
+//   scatter: same ranges, perm[position] = packet id.
+// ---------------------------------------------------------------------------------
+constexpr int kStepClasses = 16;  // class = min(nsteps, 15)
+constexpr int kSortBlock = 256;
+
+__device__ __forceinline__ uint32_t step_class(const Batch<true>& b, uint64_t p) {
+  const int32_t ns = make_geo(b.base + b.offsets[p], b.lengths[p]).nsteps;
+  return (uint32_t)(ns < kStepClasses - 1 ? ns : kStepClasses - 1);
+}
+
+__device__ __forceinline__ void sort_range(uint64_t count, uint64_t& lo, uint64_t& hi) {
+  const uint64_t per = (count + gridDim.x - 1) / gridDim.x;
+  lo = (uint64_t)blockIdx.x * per;
+  hi = lo + per < count ? lo + per : count;
+}
+
+__global__ __launch_bounds__(kSortBlock) void crc32_class_hist_kernel(Batch<true> b, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kStepClasses];
+  if (threadIdx.x < kStepClasses) h[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t lo, hi;
+  sort_range(b.count, lo, hi);
+  for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) atomicAdd(&h[step_class(b, p)], 1u);
+  __syncthreads();
+  if (threadIdx.x < kStepClasses) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(1024) void crc32_class_scan_kernel(uint32_t* __restrict__ v, uint32_t n) {
+  __shared__ uint32_t part[1024];
+  const uint32_t per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += v[i];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the partial sums
+    const uint32_t add = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += add;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - sum;
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+}
+
+__global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<true> b, const uint32_t* __restrict__ first,
+                                                                          uint32_t* __restrict__ perm) {
+  __shared__ uint32_t cur[kStepClasses];
+  if (threadIdx.x < kStepClasses) cur[threadIdx.x] = first[threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  uint64_t lo, hi;
+  sort_range(b.count, lo, hi);
+  for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) perm[atomicAdd(&cur[step_class(b, p)], 1u)] = (uint32_t)p;
 }
 
 // ---------------------------------------------------------------------------------
@@ -594,33 +673,22 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, u
 // load_top_words only when the chunk would reach below the caller's base.
 // ---------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void LdsVoid;
-constexpr int kDmaRing = 5;                                  // LDS slots per wave
-constexpr int kDmaRounds = 1;                                // rounds interleaved per wave
+constexpr int kDmaRing = 4;                                  // LDS slots per wave
 constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
 
-// Wait until at most N DMAs are outstanding, read W landed slots (16 B per lane each),
-// and wait for the reads (the slots are refilled right after).
-template <int N, int W>
-__device__ __forceinline__ void read_landed_slots(const uint32_t (&addr)[W], u32x4 (&v)[W]) {
-  if constexpr (W == 1) {
-    asm volatile(
-        "s_waitcnt vmcnt(%1)\n\t"
-        "ds_read_b128 %0, %2\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=v"(v[0])
-        : "i"(N), "v"(addr[0])
-        : "memory");
-  } else {
-    static_assert(W == 2, "1 or 2 interleaved rounds");
-    asm volatile(
-        "s_waitcnt vmcnt(%2)\n\t"
-        "ds_read_b128 %0, %3\n\t"
-        "ds_read_b128 %1, %4\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1])
-        : "i"(N), "v"(addr[0]), "v"(addr[1])
-        : "memory");
-  }
+// Wait until at most N DMAs are outstanding, read the landed slot (16 B per lane),
+// and wait for the read (the slot is refilled right after).
+template <int N>
+__device__ __forceinline__ u32x4 read_landed_slot(uint32_t addr) {
+  u32x4 v;
+  asm volatile(
+      "s_waitcnt vmcnt(%1)\n\t"
+      "ds_read_b128 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(v)
+      : "i"(N), "v"(addr)
+      : "memory");
+  return v;
 }
 
 // The 8 groups' trailing-byte words, via the scalar unit (a vector load here would
@@ -651,25 +719,45 @@ __device__ __forceinline__ uint32_t tail_words_scalar(const uint64_t (&a)[8], ui
   return w;
 }
 
-// W rounds (8W packets) are processed together: W independent sets of 4 Horner
-// chains per lane, so each wait on the LDS lookups covers twice the work.
-template <int NS, bool kTail, int W>
+// LDS atomic add in asm: hipcc would otherwise order it behind every in-flight LDS-DMA
+// (it cannot tell the counter from the ring) and drain the ring with vmcnt(0).
+__device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
+  uint32_t old;
+  const uint32_t addr = (uint32_t)(uintptr_t)(LdsVoid*)counter, one = 1;
+  asm volatile(
+      "ds_add_rtn_u32 %0, %1, %2\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(old)
+      : "v"(addr), "v"(one)
+      : "memory");
+  return old;
+}
+
+// Work distribution.  Workgroup b owns the rounds b*16 + j + i*16*gridDim (j < 16),
+// i.e. the whole grid sweeps the batch front to back together.  Inside the workgroup
+// the waves take those rounds in order from an LDS counter instead of statically:
+// the SIMD arbiter favours older waves, and with a static split the youngest waves of
+// a CU finished up to 1.5x later than the oldest, leaving the CU
+// half-occupied at the end.  A wave knows its next kLook rounds ahead of time (the
+// ring prefetches that far) and fetches one more per round.
+template <int NS, bool kTail>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
-  static_assert(kDmaRing > W, "ring must hold more than one step");
+  __shared__ uint32_t next_dispatch;
+  constexpr int kLook = 1 + (NS - 1 + kDmaRing) / NS;  // rounds a wave must know ahead
+  if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
   fill_lds(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(u.base);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wv);
-  const uint64_t first = (uint64_t)wave * kPacketsPerWave;
-  const uint64_t P = (uint64_t)gridDim.x * kWavesPerBlock * kPacketsPerWave;
-  if (first >= u.count) return;
-  const uint64_t nrounds = (u.count - first + P - 1) / P;
-  const uint64_t nsuper = (nrounds + W - 1) / W;
+  const uint64_t total_rounds = (u.count + kPacketsPerWave - 1) / kPacketsPerWave;
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto round_of = [&](uint32_t d) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
 
   const PacketGeo g = make_geo(0, u.length);
   // This lane's slot-0 chunk relative to its packet's start (> -128: DESIGN.md §3).
@@ -685,12 +773,12 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;  // round_meta()'s head field
   const uint32_t ntail = u.length & 3u;
 
-  // Round rho of this wave: packets first + rho*P + (0..7).
-  auto packet_index = [&](uint64_t rho, uint32_t grp) -> uint64_t {
-    const uint64_t p = first + rho * P + grp;
-    return p < u.count ? p : u.count - 1;  // lanes past the end re-read the last packet, never store
+  // Packet of group `grp` in round `rnd`; rounds past the end re-read the last packet.
+  auto packet_index = [&](uint64_t rnd, uint32_t grp) -> uint64_t {
+    const uint64_t p = rnd * kPacketsPerWave + grp;
+    return p < u.count ? p : u.count - 1;
   };
-  auto packet_base = [&](uint64_t rho) -> uint64_t { return u.base + packet_index(rho, c.grp) * u.stride; };
+  auto packet_base = [&](uint64_t rnd) -> uint64_t { return u.base + packet_index(rnd, c.grp) * u.stride; };
   auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
   auto slot_src = [&](uint64_t pb, int s) -> uint64_t {
     if (s != 0) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * s);
@@ -701,88 +789,72 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   auto dma = [&](uint64_t src, uint32_t q) {
     __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 0);
   };
-  // DMA unit i of super-round r (i = s*W + w): slot s of round r*W + w.
-  constexpr int kUnits = NS * W;
-  auto unit_src = [&](uint64_t r, int i) -> uint64_t {
-    const uint64_t rr = r + (uint64_t)(i / kUnits);
-    const int rem = i % kUnits;
-    return slot_src(packet_base(rr * W + (uint64_t)(rem % W)), rem / W);
-  };
 
+  uint64_t rnd[kLook + 1];  // rnd[0]: current round; rnd[i]: i rounds ahead (wave-uniform)
 #pragma unroll
-  for (int f = 0; f < kDmaRing; ++f) dma(unit_src(0, f), (uint32_t)f);
-  uint32_t q = 0;  // ring position of the next unit to consume (wave-uniform)
-  uint32_t res = 0;
-  for (uint64_t r = 0; r < nsuper; ++r) {
-    uint64_t pb[W];
-    uint32_t tw[W];
+  for (int i = 0; i < kLook; ++i) rnd[i] = round_of(wv + (uint32_t)(kWavesPerBlock * i));
+  if (rnd[0] >= total_rounds) return;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      pb[w] = packet_base(r * W + w);
-      tw[w] = 0;
-      if constexpr (kTail) {
-        uint64_t ta[8];
+  for (int f = 0; f < kDmaRing; ++f) dma(slot_src(packet_base(rnd[f / NS]), f % NS), (uint32_t)f);
+  uint32_t q = 0;  // ring position of the next slot to consume (wave-uniform)
+  uint32_t res = 0, j = 0;
+  uint64_t res_round = 0;
+  while (rnd[0] < total_rounds) {
+    // Claim the round kLook ahead; its index is first needed one round from now.
+    uint32_t d = 0;
+    if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
+    const uint64_t pb = packet_base(rnd[0]);
+    uint32_t tw = 0;
+    if constexpr (kTail) {
+      uint64_t ta[8];
 #pragma unroll
-        for (uint32_t gi = 0; gi < 8; ++gi) ta[gi] = u.base + packet_index(r * W + w, gi) * u.stride + g.a1;
-        tw[w] = tail_words_scalar(ta, c.grp);
-      }
+      for (uint32_t gi = 0; gi < 8; ++gi) ta[gi] = u.base + packet_index(rnd[0], gi) * u.stride + g.a1;
+      tw = tail_words_scalar(ta, c.grp);
     }
-    uint32_t h[W][4];
+    uint32_t h0, h1, h2, h3;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      uint32_t addr[W];
-      u32x4 v[W];
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const uint32_t qw = q + w < (uint32_t)kDmaRing ? q + w : q + w - kDmaRing;
-        addr[w] = ring0 + qw * kRingStride + lane * 16u;
+      const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
+      {
+        const int f = s + kDmaRing;  // slot f % NS of round rnd[f / NS]
+        dma(slot_src(packet_base(rnd[f / NS]), f % NS), q);
       }
-      read_landed_slots<kDmaRing - W, W>(addr, v);
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const uint32_t qw = q + w < (uint32_t)kDmaRing ? q + w : q + w - kDmaRing;
-        dma(unit_src(r, s * W + w + kDmaRing), qw);
-      }
-      q = q + W < (uint32_t)kDmaRing ? q + W : q + W - kDmaRing;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        uint32_t w0 = v[w].x, w1 = v[w].y, w2 = v[w].z, w3 = v[w].w;
-        if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
-          const bool below = is_below(pb[w]);
-          if (__builtin_amdgcn_ballot_w64(below)) {
-            if (below) load_top_words(pb[w] + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
-          }
-          h[w][0] = (w0 & am[0]) ^ xm[0];
-          h[w][1] = (w1 & am[1]) ^ xm[1];
-          h[w][2] = (w2 & am[2]) ^ xm[2];
-          h[w][3] = (w3 & am[3]) ^ xm[3];
-        } else {
-          h[w][0] = horner_main(lds, h[w][0], w0, c.lk);
-          h[w][1] = horner_main(lds, h[w][1], w1, c.lk);
-          h[w][2] = horner_main(lds, h[w][2], w2, c.lk);
-          h[w][3] = horner_main(lds, h[w][3], w3, c.lk);
+      q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
+      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+      if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
+        const bool below = is_below(pb);
+        if (__builtin_amdgcn_ballot_w64(below)) {
+          if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
         }
+        h0 = (w0 & am[0]) ^ xm[0];
+        h1 = (w1 & am[1]) ^ xm[1];
+        h2 = (w2 & am[2]) ^ xm[2];
+        h3 = (w3 & am[3]) ^ xm[3];
+      } else {
+        h0 = horner_main(lds, h0, w0, c.lk);
+        h1 = horner_main(lds, h1, w1, c.lk);
+        h2 = horner_main(lds, h2, w2, c.lk);
+        h3 = horner_main(lds, h3, w3, c.lk);
       }
-      issue_order_fence();  // keep each step's lookups between its DMAs and the next step's wait
+      issue_order_fence();  // keep each slot's lookups between its DMA and the next slot's wait
     }
-    uint32_t crc[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint32_t reg = combine_streams(lds, h[w][0], h[w][1], h[w][2], h[w][3]);
-      if constexpr (kTail) reg = tail_steps(lds, reg, tw[w], ntail, 0);
-      crc[w] = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
+    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    // Lane 8g+j keeps the checksum of group g in this wave's j-th round of 8; one store per 8.
+    if (c.k == j) {
+      res = crc;
+      res_round = rnd[0];
     }
-    // Lane 8g+j keeps round (rho & ~7) + j's checksum of group g; one store per 8 rounds.
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const uint64_t rho = r * W + w;
-      if (W > 1 && rho >= nrounds) break;
-      const uint32_t j = (uint32_t)(rho & 7u);
-      if (c.k == j) res = crc[w];
-      if (j == 7u || rho + 1 == nrounds) {
-        const uint64_t p = first + (rho - j + c.k) * P + c.grp;
-        if (c.k <= j && p < u.count) out[p] = res;
-      }
+    for (int i = 0; i < kLook - 1; ++i) rnd[i] = rnd[i + 1];
+    rnd[kLook - 1] = round_of(__builtin_amdgcn_readfirstlane(d));
+    if (j == 7u || rnd[0] >= total_rounds) {
+      const uint64_t p = res_round * kPacketsPerWave + c.grp;
+      if (c.k <= j && p < u.count) out[p] = res;
+      j = 0;
+    } else {
+      ++j;
     }
   }
   // The ring's last DMAs (re-reads of valid packets) must land before the wave's LDS goes away.
@@ -838,8 +910,7 @@ template <int NS, bool kTail>
 static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks,
                                    bool dma) {
   if (dma)
-    hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS, kTail, kDmaRounds>), dim3(blocks), dim3(kBlock), 0, stream, u,
-                       out);
+    hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   else
     hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
@@ -915,14 +986,39 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   return L.streaming();
 }
 
+// Below this many packets the sort costs more than the padding it saves.
+constexpr uint64_t kSortMinPackets = 4096;
+
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
                          uint64_t count, uint32_t* out, hipStream_t stream) {
   if (count == 0) return hipSuccess;
   hipError_t err;
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
-  Launcher<true> L{Batch<true>{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count}, out, stream, blocks};
-  return L.streaming();
+  Batch<true> b{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count};
+  if (count < kSortMinPackets || count > 0xFFFFFFFFull) {
+    Launcher<true> L{b, out, stream, blocks};
+    return L.streaming();
+  }
+  // Scratch in stream order: histogram/scan array, then the permutation.
+  uint64_t sort_blocks = (count + 4 * kSortBlock - 1) / (4 * kSortBlock);
+  sort_blocks = sort_blocks < 1024 ? sort_blocks : 1024;  // scan: <= 16 entries per thread
+  const size_t hist_bytes = ((size_t)kStepClasses * sort_blocks * 4 + 255) & ~(size_t)255;
+  void* scratch = nullptr;
+  err = hipMallocAsync(&scratch, hist_bytes + (size_t)count * 4, stream);
+  if (err != hipSuccess) return err;
+  uint32_t* hist = static_cast<uint32_t*>(scratch);
+  uint32_t* perm = reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + hist_bytes);
+  hipLaunchKernelGGL(crc32_class_hist_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b, hist);
+  hipLaunchKernelGGL(crc32_class_scan_kernel, dim3(1), dim3(1024), 0, stream, hist,
+                     (uint32_t)(kStepClasses * sort_blocks));
+  hipLaunchKernelGGL(crc32_class_scatter_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
+                     (const uint32_t*)hist, perm);
+  b.perm = perm;
+  Launcher<true> L{b, out, stream, blocks};
+  err = L.streaming();
+  const hipError_t ferr = hipFreeAsync(scratch, stream);
+  return err != hipSuccess ? err : ferr;
 }
 
 }  // namespace enet_crc

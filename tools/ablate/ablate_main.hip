@@ -29,7 +29,7 @@ int main(int argc, char** argv) {
 #ifdef STAMPS
   // Per-wave cycle stamps of the last launch: ring wait (vmcnt), ring read (ds_read_b128),
   // combine, and the whole loop (s_memtime units).
-  static unsigned long long st[5 * 8192];
+  static unsigned long long st[6 * 8192];
   hipMemcpyFromSymbol(st, HIP_SYMBOL(enet_crc::g_stamp), sizeof(st));
   double sum[4] = {0, 0, 0, 0}, rt = 0;
   int nw = 0;
@@ -38,6 +38,36 @@ int main(int argc, char** argv) {
     ++nw;
     for (int j = 0; j < 4; ++j) sum[j] += st[4 * w + j];
     rt += st[32768 + w];
+  }
+  {
+    unsigned long long s0 = ~0ull, s1 = 0, e1 = 0, e0 = ~0ull, dmin = ~0ull, dmax = 0;
+    for (int w = 0; w < 8192; ++w) {
+      if (st[4 * w + 3] == 0) continue;
+      const unsigned long long a = st[40960 + w], d = st[32768 + w], e = a + d;
+      s0 = a < s0 ? a : s0; s1 = a > s1 ? a : s1; e0 = e < e0 ? e : e0; e1 = e > e1 ? e : e1;
+      dmin = d < dmin ? d : dmin; dmax = d > dmax ? d : dmax;
+    }
+    if (nw) printf("  loop start spread %.1f us, end spread %.1f us (first end %.1f, last end %.1f us after first start), loop min %.1f max %.1f us\n",
+                   (s1 - s0) * 0.01, (e1 - e0) * 0.01, (e0 - s0) * 0.01, (e1 - s0) * 0.01, dmin * 0.01, dmax * 0.01);
+  }
+  {
+    // Wave end times grouped by XCD (workgroup b runs on XCD b % 8).
+    unsigned long long s0 = ~0ull;
+    for (int w = 0; w < 8192; ++w)
+      if (st[4 * w + 3] && st[40960 + w] < s0) s0 = st[40960 + w];
+    double sum_x[8] = {0}, max_x[8] = {0}, min_x[8] = {1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30};
+    int n_x[8] = {0};
+    for (int w = 0; w < 8192; ++w) {
+      if (st[4 * w + 3] == 0) continue;
+      const int x = (w / 16) % 8;
+      const double e = (st[40960 + w] + st[32768 + w] - s0) * 0.01;
+      sum_x[x] += e; ++n_x[x];
+      max_x[x] = e > max_x[x] ? e : max_x[x];
+      min_x[x] = e < min_x[x] ? e : min_x[x];
+    }
+    printf("  end time by XCD (mean/min/max us):");
+    for (int x = 0; x < 8; ++x) if (n_x[x]) printf(" %d:%.0f/%.0f/%.0f", x, sum_x[x] / n_x[x], min_x[x], max_x[x]);
+    printf("\n");
   }
   if (nw) printf("  in-kernel clock %.2f GHz (s_memtime / s_memrealtime x 100 MHz), loop %.1f us per wave\n",
                  sum[3] / rt * 0.1, rt / nw * 0.01);

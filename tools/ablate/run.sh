@@ -32,27 +32,26 @@ build base
 build no_lookup "$NO_LOOKUP"
 build no_mem "$DMA_NOMEM" "$REGS_NOMEM1" "$REGS_NOMEM2"
 build no_lookup_no_mem "$NO_LOOKUP" "$DMA_NOMEM" "$REGS_NOMEM1" "$REGS_NOMEM2"
-build ring4 'constexpr int kDmaRing = 5; =>constexpr int kDmaRing = 4; '
-build comb_trivial 'uint32_t reg = combine_streams(lds, h[w][0], h[w][1], h[w][2], h[w][3]);=>uint32_t reg = h[w][0] ^ h[w][1] ^ h[w][2] ^ h[w][3];'
-build w2 'constexpr int kDmaRounds = 1; =>constexpr int kDmaRounds = 2; '
+build comb_trivial 'uint32_t reg = combine_streams(lds, h0, h1, h2, h3);=>uint32_t reg = h0 ^ h1 ^ h2 ^ h3;'
 STAMP1='__device__ const OpTables g_op_tables = kOpTables;=>__device__ const OpTables g_op_tables = kOpTables;
 #define STAMPS 1
-__device__ unsigned long long g_stamp[5 * 8192];'
-STAMP2='read_landed_slots<kDmaRing - W, W>(addr, v);=>const uint64_t st0 = __builtin_readcyclecounter(); uint64_t st1;
-      asm volatile("s_waitcnt vmcnt(%2)\n\ts_memtime %1\n\tds_read_b128 %0, %3\n\ts_waitcnt lgkmcnt(0)" : "=v"(v[0]), "=&s"(st1) : "i"(kDmaRing - 1), "v"(addr[0]) : "memory");
+__device__ unsigned long long g_stamp[6 * 8192];'
+STAMP2='const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);=>const uint64_t st0 = __builtin_readcyclecounter(); uint64_t st1; u32x4 v;
+      asm volatile("s_waitcnt vmcnt(%2)\n\ts_memtime %1\n\tds_read_b128 %0, %3\n\ts_waitcnt lgkmcnt(0)" : "=v"(v), "=&s"(st1) : "i"(kDmaRing - 1), "v"(ring0 + q * kRingStride + lane * 16u) : "memory");
       t_vm += st1 - st0; t_ds += __builtin_readcyclecounter() - st1;'
-STAMP3='uint32_t res = 0;
-  for (uint64_t r = 0; r < nsuper; ++r) {=>uint32_t res = 0; uint64_t t_vm = 0, t_ds = 0, t_comb = 0; const uint64_t t_start = __builtin_readcyclecounter(); const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
-  for (uint64_t r = 0; r < nsuper; ++r) {'
-STAMP4='    uint32_t crc[W];=>    const uint64_t sc0 = __builtin_readcyclecounter();
-    uint32_t crc[W];'
-STAMP5='    // Lane 8g+j keeps round=>    t_comb += __builtin_readcyclecounter() - sc0;
-    // Lane 8g+j keeps round'
+STAMP3='uint32_t res = 0, j = 0;=>uint32_t res = 0, j = 0; uint64_t t_vm = 0, t_ds = 0, t_comb = 0; const uint64_t t_start = __builtin_readcyclecounter(); const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();'
+STAMP4='    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
+    const uint32_t crc=>    const uint64_t sc0 = __builtin_readcyclecounter();
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
+    const uint32_t crc'
+STAMP5='    // Lane 8g+j keeps the checksum=>    t_comb += __builtin_readcyclecounter() - sc0;
+    // Lane 8g+j keeps the checksum'
 STAMP6='  __builtin_amdgcn_s_waitcnt(0);
-}=>  if (lane == 0) { g_stamp[wave * 4] = t_vm; g_stamp[wave * 4 + 1] = t_ds; g_stamp[wave * 4 + 2] = t_comb; g_stamp[wave * 4 + 3] = __builtin_readcyclecounter() - t_start; g_stamp[32768 + wave] = __builtin_amdgcn_s_memrealtime() - rt_start; }
+}=>  { const uint32_t wave = blockIdx.x * 16 + wv; if (lane == 0) { g_stamp[wave * 4] = t_vm; g_stamp[wave * 4 + 1] = t_ds; g_stamp[wave * 4 + 2] = t_comb; g_stamp[wave * 4 + 3] = __builtin_readcyclecounter() - t_start; g_stamp[32768 + wave] = __builtin_amdgcn_s_memrealtime() - rt_start; g_stamp[40960 + wave] = rt_start; } }
   __builtin_amdgcn_s_waitcnt(0);
 }'
 build stamps "$STAMP1" "$STAMP2" "$STAMP3" "$STAMP4" "$STAMP5" "$STAMP6"
 build stamps_no_mem "$STAMP1" "$STAMP2" "$STAMP3" "$STAMP4" "$STAMP5" "$STAMP6" "$DMA_NOMEM"
-build stamps_no_lookup "$STAMP1" "$STAMP2" "$STAMP3" "$STAMP4" "$STAMP5" "$STAMP6" "$NO_LOOKUP"
 ls -la bin
