@@ -740,12 +740,15 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 // a CU finished up to 1.5x later than the oldest, leaving the CU
 // half-occupied at the end.  A wave knows its next kLook rounds ahead of time (the
 // ring prefetches that far) and fetches one more per round.
+// NS > 0: packets of exactly NS steps, the slot loop fully unrolled.  NS == 0: any
+// step count >= kDmaRing (long packets, e.g. 64 KiB buffers: 512 steps), slot loop
+// unrolled by the ring depth.
 template <int NS, bool kTail>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
   __shared__ uint32_t next_dispatch;
-  constexpr int kLook = 1 + (NS - 1 + kDmaRing) / NS;  // rounds a wave must know ahead
+  constexpr int kLook = NS > 0 ? 1 + (NS - 1 + kDmaRing) / NS : 2;  // rounds a wave must know ahead
   if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
   fill_lds(lds);
   __syncthreads();
@@ -760,8 +763,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   };
 
   const PacketGeo g = make_geo(0, u.length);
+  const int32_t ns = NS > 0 ? NS : g.nsteps;
   // This lane's slot-0 chunk relative to its packet's start (> -128: DESIGN.md §3).
-  const int64_t rel0 = (int64_t)g.a1 - 16 * (int64_t)(c.k + 1u) - (int64_t)kBytesPerStep * (NS - 1);
+  const int64_t rel0 = (int64_t)g.a1 - 16 * (int64_t)(c.k + 1u) - (int64_t)kBytesPerStep * (ns - 1);
   uint32_t am[4], xm[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -780,7 +784,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   };
   auto packet_base = [&](uint64_t rnd) -> uint64_t { return u.base + packet_index(rnd, c.grp) * u.stride; };
   auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
-  auto slot_src = [&](uint64_t pb, int s) -> uint64_t {
+  auto slot_src = [&](uint64_t pb, int32_t s) -> uint64_t {
     if (s != 0) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * s);
     return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
   };
@@ -795,7 +799,12 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   for (int i = 0; i < kLook; ++i) rnd[i] = round_of(wv + (uint32_t)(kWavesPerBlock * i));
   if (rnd[0] >= total_rounds) return;
 #pragma unroll
-  for (int f = 0; f < kDmaRing; ++f) dma(slot_src(packet_base(rnd[f / NS]), f % NS), (uint32_t)f);
+  for (int f = 0; f < kDmaRing; ++f) {
+    if constexpr (NS > 0)
+      dma(slot_src(packet_base(rnd[f / NS]), f % NS), (uint32_t)f);
+    else
+      dma(slot_src(packet_base(rnd[0]), f), (uint32_t)f);  // ns >= kDmaRing
+  }
   uint32_t q = 0;  // ring position of the next slot to consume (wave-uniform)
   uint32_t res = 0, j = 0;
   uint64_t res_round = 0;
@@ -804,6 +813,8 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
     uint32_t d = 0;
     if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
     const uint64_t pb = packet_base(rnd[0]);
+    uint64_t pb_next = 0;
+    if constexpr (NS == 0) pb_next = packet_base(rnd[1]);
     uint32_t tw = 0;
     if constexpr (kTail) {
       uint64_t ta[8];
@@ -811,17 +822,18 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
       for (uint32_t gi = 0; gi < 8; ++gi) ta[gi] = u.base + packet_index(rnd[0], gi) * u.stride + g.a1;
       tw = tail_words_scalar(ta, c.grp);
     }
-    uint32_t h0, h1, h2, h3;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    // One slot: wait for it, refill its LDS slot kDmaRing slots ahead, then the lookups.
+    auto slot = [&](int32_t s, bool top) {
       const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
-      {
-        const int f = s + kDmaRing;  // slot f % NS of round rnd[f / NS]
-        dma(slot_src(packet_base(rnd[f / NS]), f % NS), q);
-      }
+      const int32_t f = s + kDmaRing;
+      if constexpr (NS > 0)
+        dma(slot_src(packet_base(rnd[f / NS]), f % NS), q);  // f / NS, f % NS fold to constants
+      else
+        dma(f < ns ? slot_src(pb, f) : slot_src(pb_next, f - ns), q);
       q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
       uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-      if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
+      if (top) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
         const bool below = is_below(pb);
         if (__builtin_amdgcn_ballot_w64(below)) {
           if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
@@ -837,6 +849,13 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
         h3 = horner_main(lds, h3, w3, c.lk);
       }
       issue_order_fence();  // keep each slot's lookups between its DMA and the next slot's wait
+    };
+    if constexpr (NS > 0) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) slot(s, s == 0);
+    } else {
+      slot(0, true);
+      for (int32_t s = 1; s < ns; ++s) slot(s, false);
     }
     uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
     if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
@@ -943,6 +962,16 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   hipError_t err;
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
   const int ns = make_geo(0, length).nsteps;
+  if (((b0 | stride) & 3u) == 0 && ns > kMaxRoundSteps && use_dma_uniform()) {  // long packets
+    const unsigned blocks = grid_for(count, err);
+    if (err != hipSuccess) return err;
+    const UniformBatch u{b0, stride, length, count};
+    if (length & 3u)
+      hipLaunchKernelGGL((crc32_uniform_dma_kernel<0, true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+    else
+      hipLaunchKernelGGL((crc32_uniform_dma_kernel<0, false>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+    return hipGetLastError();
+  }
   if (((b0 | stride) & 3u) == 0 && ns >= 1 && ns <= kMaxRoundSteps) {
     const bool tail = (length & 3u) != 0;
     if (use_dma_uniform()) {  // one launch covers the whole batch
