@@ -558,6 +558,29 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<t
   for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) perm[atomicAdd(&cur[step_class(b, p)], 1u)] = (uint32_t)p;
 }
 
+// Round records for crc32_ragged_dma_kernel: sorted position q = 8 r + g goes to
+// record r, group g.  128 B per round: start addresses (u64 x 8), lengths (u32 x 8),
+// packet ids (u32 x 8).
+constexpr uint32_t kRecordBytes = 128;
+constexpr uint32_t kRecLenOff = 64, kRecIdOff = 96;
+
+__global__ __launch_bounds__(kSortBlock) void crc32_class_records_kernel(Batch<true> b, const uint32_t* __restrict__ first,
+                                                                          uint8_t* __restrict__ recs) {
+  __shared__ uint32_t cur[kStepClasses];
+  if (threadIdx.x < kStepClasses) cur[threadIdx.x] = first[threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
+  uint64_t lo, hi;
+  sort_range(b.count, lo, hi);
+  for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) {
+    const uint64_t q = atomicAdd(&cur[step_class(b, p)], 1u);
+    uint8_t* r = recs + (q / kPacketsPerWave) * kRecordBytes;
+    const uint32_t g = (uint32_t)(q % kPacketsPerWave);
+    reinterpret_cast<uint64_t*>(r)[g] = b.base + b.offsets[p];
+    reinterpret_cast<uint32_t*>(r + kRecLenOff)[g] = b.lengths[p];
+    reinterpret_cast<uint32_t*>(r + kRecIdOff)[g] = (uint32_t)p;
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Uniform kernel: a uniform batch whose base and stride are multiples of 4, so every
 // packet has the same geometry relative to its own start.  Per-lane chunk offsets,
@@ -880,6 +903,181 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   __builtin_amdgcn_s_waitcnt(0);
 }
 
+// ---------------------------------------------------------------------------------
+// Ragged kernel, LDS-DMA form.  Packets come sorted by step class (round records from
+// crc32_class_records_kernel), so the 8 packets of a round need (nearly) the same
+// number of slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the
+// packets with fewer steps read the zero chunk in their leading slots.  Same ring,
+// dispatch and waits as crc32_uniform_dma_kernel, with per-round, per-lane geometry
+// (streaming kernel's round_meta/mask_top/fallback logic).  Three more DMA kinds join
+// the vector-memory stream, each issued at least kDmaRing-1 DMAs before it is read:
+//   - round records (4 B per lane: the 128-B record, lanes 32-63 duplicate it), two
+//     rounds ahead, read with ds_read at the previous round's end;
+//   - the trailing-byte words (4 B per lane, lane 0 of each group), at the round's
+//     start, read at its end.
+// ---------------------------------------------------------------------------------
+struct RaggedDmaBatch {
+  uint64_t base;        // caller's buffer (fallback bound)
+  const uint8_t* recs;  // round records
+  uint64_t count;
+};
+
+struct RaggedRound {
+  uint64_t cb;          // this lane's chunk address at slot 0
+  uint64_t tail_addr;   // word holding the trailing bytes, or the zero chunk
+  int32_t ns;           // slots of the round (wave-uniform)
+  int32_t top_slot;     // slot of this lane's top chunk (ns: packet has no whole word)
+  uint32_t meta;        // round_meta()
+  uint32_t id;          // packet id (output index)
+  bool direct;          // top chunk read directly (not fallback / not before the packet)
+};
+
+__device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint64_t& addr, uint32_t& len,
+                                            uint32_t& id) {
+  const uint32_t a = rec_lds + 8u * grp, l = rec_lds + kRecLenOff + 4u * grp, i = rec_lds + kRecIdOff + 4u * grp;
+  asm volatile(
+      "ds_read_b64 %0, %3\n\t"
+      "ds_read_b32 %1, %4\n\t"
+      "ds_read_b32 %2, %5\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(addr), "=&v"(len), "=&v"(id)
+      : "v"(a), "v"(l), "v"(i)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t read_lds_word(uint32_t lds_addr) {
+  uint32_t v;
+  asm volatile(
+      "ds_read_b32 %0, %1\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(v)
+      : "v"(lds_addr)
+      : "memory");
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch b, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
+  __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
+  __shared__ __attribute__((aligned(16))) uint32_t recb[2][kWavesPerBlock][64];
+  __shared__ __attribute__((aligned(16))) uint32_t tailb[kWavesPerBlock][64];
+  __shared__ uint32_t next_dispatch;
+  constexpr int kLook = 3;
+  if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(b.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const uint64_t total_rounds = (b.count + kPacketsPerWave - 1) / kPacketsPerWave;
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto round_of = [&](uint32_t d) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
+  auto dma16 = [&](uint64_t src, uint32_t q) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 0);
+  };
+  auto dma_record = [&](uint64_t rnd, uint32_t buf) {
+    const uint64_t r = rnd < total_rounds ? rnd : total_rounds - 1;
+    const uint64_t src = (uint64_t)(uintptr_t)b.recs + r * kRecordBytes + 4u * (lane & 31u);
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&recb[buf][wv][0], 4, 0, 0);
+  };
+  auto make_round = [&](uint64_t rnd, uint32_t buf) -> RaggedRound {
+    uint64_t sa;
+    uint32_t len, id;
+    read_record((uint32_t)(uintptr_t)(LdsVoid*)&recb[buf][wv][0], c.grp, sa, len, id);
+    const bool valid = rnd < total_rounds && rnd * kPacketsPerWave + c.grp < b.count;
+    if (!valid) {
+      sa = c.base4;
+      len = 0;
+    }
+    const PacketGeo g = make_geo(sa, len);
+    RaggedRound rr;
+    rr.ns = max(kDmaRing, wave_max_over_groups(g.nsteps));
+    rr.cb = g.a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
+    rr.top_slot = rr.ns - g.nsteps;
+    rr.direct = g.nsteps > 0 && chunk_kind(g, c.k, g.nsteps - 1, c.base4) == kChunkDirect;
+    rr.meta = round_meta(g, c.k, c.base4, valid, rr.tail_addr, c.dummy);
+    rr.id = id;
+    return rr;
+  };
+  auto unit_src = [&](const RaggedRound& rr, int32_t s) -> uint64_t {
+    const bool real = s > rr.top_slot || (s == rr.top_slot && rr.direct);
+    return real ? rr.cb + (uint64_t)kBytesPerStep * (uint64_t)s : c.dummy;
+  };
+
+  uint64_t rnd[kLook + 1];
+#pragma unroll
+  for (int i = 0; i < kLook; ++i) rnd[i] = round_of(wv + (uint32_t)(kWavesPerBlock * i));
+  if (rnd[0] >= total_rounds) return;
+  dma_record(rnd[0], 0);
+  dma_record(rnd[1], 1);
+  __builtin_amdgcn_s_waitcnt(0);  // prologue only: both records landed (no other LDS-DMA yet)
+  RaggedRound cur = make_round(rnd[0], 0);
+  RaggedRound nxt = make_round(rnd[1], 1);
+  dma_record(rnd[2], 0);  // read one round from now
+#pragma unroll
+  for (int f = 0; f < kDmaRing; ++f) dma16(unit_src(cur, f), (uint32_t)f);  // cur.ns >= kDmaRing
+  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
+  const uint32_t tail_lds = (uint32_t)(uintptr_t)(LdsVoid*)&tailb[wv][lane];
+  uint32_t q = 0;
+  uint32_t res = 0, res_id = 0, j = 0;
+  bool res_valid = false;
+  while (rnd[0] < total_rounds) {
+    uint32_t d = 0;
+    if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
+    __builtin_amdgcn_global_load_lds((const void*)cur.tail_addr, (LdsVoid*)&tailb[wv][0], 4, 0, 0);
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    for (int32_t s = 0; s < cur.ns; ++s) {
+      const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
+      const int32_t f = s + kDmaRing;
+      dma16(f < cur.ns ? unit_src(cur, f) : unit_src(nxt, f - cur.ns), q);
+      q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
+      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+      const bool top = s == cur.top_slot;
+      if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+        if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
+          if (top && (cur.meta & kMetaFallback))
+            load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
+        }
+        if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
+      }
+      h0 = horner_main(lds, h0, w0, c.lk);
+      h1 = horner_main(lds, h1, w1, c.lk);
+      h2 = horner_main(lds, h2, w2, c.lk);
+      h3 = horner_main(lds, h3, w3, c.lk);
+      issue_order_fence();
+    }
+    // Round end: the tail word and record rnd[2] have landed (>= kDmaRing-1 DMAs since).
+    const uint32_t tail_word = read_lds_word(tail_lds);
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    if (cur.meta & kMetaEmpty) reg = kInitRegister;
+    reg = tail_steps(lds, reg, tail_word, (cur.meta >> kMetaNTailShift) & 3u, (cur.meta >> kMetaTShiftShift) & 3u);
+    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    if (c.k == j) {
+      res = crc;
+      res_id = cur.id;
+      res_valid = (cur.meta & kMetaStore) != 0;
+    }
+    const RaggedRound after = make_round(rnd[2], 0);
+    rnd[3] = round_of(__builtin_amdgcn_readfirstlane(d));
+    dma_record(rnd[3], 0);  // buffer 0 is free again: rnd[2]'s record was just read
+    rnd[0] = rnd[1];
+    rnd[1] = rnd[2];
+    rnd[2] = rnd[3];
+    cur = nxt;
+    nxt = after;
+    if (j == 7u || rnd[0] >= total_rounds) {
+      if (c.k <= j && res_valid) out[res_id] = res;
+      j = 0;
+    } else {
+      ++j;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
 }  // namespace
 
 int cu_count_for_current_device();
@@ -1029,23 +1227,39 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // Scratch in stream order: histogram/scan array, then the permutation.
+  // Scratch in stream order: histogram/scan array, then the permutation or the round
+  // records.  ENET_CRC_RAGGED=stream selects the register streaming kernel (A/B runs).
+  static const bool stream_kernel = [] {
+    const char* v = getenv("ENET_CRC_RAGGED");
+    return v && strcmp(v, "stream") == 0;
+  }();
   uint64_t sort_blocks = (count + 4 * kSortBlock - 1) / (4 * kSortBlock);
   sort_blocks = sort_blocks < 1024 ? sort_blocks : 1024;  // scan: <= 16 entries per thread
   const size_t hist_bytes = ((size_t)kStepClasses * sort_blocks * 4 + 255) & ~(size_t)255;
+  const uint64_t rounds = (count + kPacketsPerWave - 1) / kPacketsPerWave;
+  const size_t tail_bytes = stream_kernel ? (size_t)count * 4 : (size_t)rounds * kRecordBytes;
   void* scratch = nullptr;
-  err = hipMallocAsync(&scratch, hist_bytes + (size_t)count * 4, stream);
+  err = hipMallocAsync(&scratch, hist_bytes + tail_bytes, stream);
   if (err != hipSuccess) return err;
   uint32_t* hist = static_cast<uint32_t*>(scratch);
-  uint32_t* perm = reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + hist_bytes);
+  uint8_t* second = static_cast<uint8_t*>(scratch) + hist_bytes;
   hipLaunchKernelGGL(crc32_class_hist_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b, hist);
   hipLaunchKernelGGL(crc32_class_scan_kernel, dim3(1), dim3(1024), 0, stream, hist,
                      (uint32_t)(kStepClasses * sort_blocks));
-  hipLaunchKernelGGL(crc32_class_scatter_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
-                     (const uint32_t*)hist, perm);
-  b.perm = perm;
-  Launcher<true> L{b, out, stream, blocks};
-  err = L.streaming();
+  if (stream_kernel) {
+    uint32_t* perm = reinterpret_cast<uint32_t*>(second);
+    hipLaunchKernelGGL(crc32_class_scatter_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
+                       (const uint32_t*)hist, perm);
+    b.perm = perm;
+    Launcher<true> L{b, out, stream, blocks};
+    err = L.streaming();
+  } else {
+    hipLaunchKernelGGL(crc32_class_records_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
+                       (const uint32_t*)hist, second);
+    const RaggedDmaBatch rb{b.base, second, count};
+    hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
+    err = hipGetLastError();
+  }
   const hipError_t ferr = hipFreeAsync(scratch, stream);
   return err != hipSuccess ? err : ferr;
 }
