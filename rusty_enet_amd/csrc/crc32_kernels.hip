@@ -82,7 +82,8 @@ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 constexpr int kMainLevel = ilog2(4 * G);  // M32^(4G) = M32^32
 constexpr int kTreeLevels = ilog2(G);
 constexpr int kSmallSets = 1 + kTreeLevels;
-constexpr uint32_t kLdsDwords = kMainDwords + kSmallSets * 1024;
+constexpr uint32_t kInvTopDword = kMainDwords + kSmallSets * 1024;  // inv_top bytes, 4 per dword
+constexpr uint32_t kLdsDwords = kInvTopDword + 64;
 static_assert(kMainLevel < kOpLevels, "operator level");
 
 __device__ __forceinline__ uint32_t load_word(uint64_t addr) { return *reinterpret_cast<GlobalU32*>(addr); }
@@ -163,6 +164,10 @@ __device__ __forceinline__ void fill_lds(uint32_t* lds) {
     const int set = x >> 10, rem = x & 1023;
     const int level = set == 0 ? 0 : set + 1;  // M32^1, then M32^(4*2^(set-1))
     lds[kMainDwords + x] = g_op_tables.op[level][rem >> 8][rem & 255];
+  }
+  if (t < 64) {
+    const uint8_t* it = g_op_tables.inv_top + 4 * t;
+    lds[kInvTopDword + t] = it[0] | (it[1] << 8) | ((uint32_t)it[2] << 16) | ((uint32_t)it[3] << 24);
   }
 }
 
@@ -291,6 +296,22 @@ __device__ __forceinline__ uint32_t tail_steps(const uint32_t* lds, uint32_t reg
 #pragma unroll
   for (uint32_t t = 0; t < 3; ++t) {
     if (t < ntail) reg = (reg >> 8) ^ sarwate[(reg ^ (word >> (8u * (tsh + t)))) & 0xffu];
+  }
+  return reg;
+}
+
+// Undo z zero-byte steps (z <= 3): the DMA kernels run every packet to the next
+// 4-byte boundary, with the z bytes past its end masked to zero, which leaves
+// M8^z(reg) in the register; M8^-1 recovers the table index from the top byte.
+__device__ __forceinline__ uint32_t unshift_zero_bytes(const uint32_t* lds, uint32_t reg, uint32_t z) {
+  const uint32_t* sarwate = lds + kMainDwords + 768;
+  const uint8_t* inv_top = reinterpret_cast<const uint8_t*>(lds + kInvTopDword);
+#pragma unroll
+  for (uint32_t t = 0; t < 3; ++t) {
+    if (t < z) {
+      const uint32_t idx = inv_top[reg >> 24];
+      reg = ((reg ^ sarwate[idx]) << 8) | idx;
+    }
   }
   return reg;
 }
@@ -505,10 +526,18 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
 constexpr int kStepClasses = 16;  // class = min(nsteps, 15)
 constexpr int kSortBlock = 256;
 
-__device__ __forceinline__ uint32_t step_class(const Batch<true>& b, uint64_t p) {
-  const int32_t ns = make_geo(b.base + b.offsets[p], b.lengths[p]).nsteps;
+__device__ __forceinline__ uint32_t step_class_of(uint64_t sa, uint32_t len) {
+  const int32_t ns = make_geo(sa, len).nsteps;
   return (uint32_t)(ns < kStepClasses - 1 ? ns : kStepClasses - 1);
 }
+
+__device__ __forceinline__ uint32_t step_class(const Batch<true>& b, uint64_t p) {
+  return step_class_of(b.base + b.offsets[p], b.lengths[p]);
+}
+
+// The sort kernels give every thread up to kSortPer packets of its block's range;
+// all their descriptors are loaded before any is used (one memory latency, not kSortPer).
+constexpr int kSortPer = 4;
 
 __device__ __forceinline__ void sort_range(uint64_t count, uint64_t& lo, uint64_t& hi) {
   const uint64_t per = (count + gridDim.x - 1) / gridDim.x;
@@ -522,16 +551,40 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_hist_kernel(Batch<true
   __syncthreads();
   uint64_t lo, hi;
   sort_range(b.count, lo, hi);
-  for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) atomicAdd(&h[step_class(b, p)], 1u);
+  for (uint64_t p0 = lo + threadIdx.x; p0 < hi; p0 += kSortBlock * kSortPer) {
+    uint64_t off[kSortPer];
+    uint32_t len[kSortPer];
+#pragma unroll
+    for (int k = 0; k < kSortPer; ++k) {
+      const uint64_t p = p0 + (uint64_t)k * kSortBlock;
+      off[k] = p < hi ? b.offsets[p] : 0;
+      len[k] = p < hi ? b.lengths[p] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kSortPer; ++k)
+      if (p0 + (uint64_t)k * kSortBlock < hi) atomicAdd(&h[step_class_of(b.base + off[k], len[k])], 1u);
+  }
   __syncthreads();
   if (threadIdx.x < kStepClasses) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
+constexpr uint32_t kScanMax = kStepClasses * 1024;  // histogram entries (<= 1024 sort blocks)
+
 __global__ __launch_bounds__(1024) void crc32_class_scan_kernel(uint32_t* __restrict__ v, uint32_t n) {
+  __shared__ uint32_t buf[kScanMax];
   __shared__ uint32_t part[1024];
+  uint32_t tmp[kStepClasses];  // coalesced loads, all in flight before the first LDS store
+#pragma unroll
+  for (uint32_t k = 0; k < kStepClasses; ++k) {
+    const uint32_t i = threadIdx.x + k * 1024;
+    tmp[k] = i < n ? v[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kStepClasses; ++k) buf[threadIdx.x + k * 1024] = tmp[k];
+  __syncthreads();
   const uint32_t per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
   uint32_t sum = 0;
-  for (uint32_t i = lo; i < hi; ++i) sum += v[i];
+  for (uint32_t i = lo; i < hi; ++i) sum += buf[i];
   part[threadIdx.x] = sum;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the partial sums
@@ -542,10 +595,12 @@ __global__ __launch_bounds__(1024) void crc32_class_scan_kernel(uint32_t* __rest
   }
   uint32_t run = part[threadIdx.x] - sum;
   for (uint32_t i = lo; i < hi; ++i) {
-    const uint32_t x = v[i];
-    v[i] = run;
+    const uint32_t x = buf[i];
+    buf[i] = run;
     run += x;
   }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += 1024) v[i] = buf[i];
 }
 
 __global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<true> b, const uint32_t* __restrict__ first,
@@ -571,13 +626,27 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_records_kernel(Batch<t
   __syncthreads();
   uint64_t lo, hi;
   sort_range(b.count, lo, hi);
-  for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) {
-    const uint64_t q = atomicAdd(&cur[step_class(b, p)], 1u);
-    uint8_t* r = recs + (q / kPacketsPerWave) * kRecordBytes;
-    const uint32_t g = (uint32_t)(q % kPacketsPerWave);
-    reinterpret_cast<uint64_t*>(r)[g] = b.base + b.offsets[p];
-    reinterpret_cast<uint32_t*>(r + kRecLenOff)[g] = b.lengths[p];
-    reinterpret_cast<uint32_t*>(r + kRecIdOff)[g] = (uint32_t)p;
+  for (uint64_t p0 = lo + threadIdx.x; p0 < hi; p0 += kSortBlock * kSortPer) {
+    uint64_t off[kSortPer];
+    uint32_t len[kSortPer];
+#pragma unroll
+    for (int k = 0; k < kSortPer; ++k) {
+      const uint64_t p = p0 + (uint64_t)k * kSortBlock;
+      off[k] = p < hi ? b.offsets[p] : 0;
+      len[k] = p < hi ? b.lengths[p] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kSortPer; ++k) {
+      const uint64_t p = p0 + (uint64_t)k * kSortBlock;
+      if (p >= hi) continue;
+      const uint64_t sa = b.base + off[k];
+      const uint64_t q = atomicAdd(&cur[step_class_of(sa, len[k])], 1u);
+      uint8_t* r = recs + (q / kPacketsPerWave) * kRecordBytes;
+      const uint32_t g = (uint32_t)(q % kPacketsPerWave);
+      reinterpret_cast<uint64_t*>(r)[g] = sa;
+      reinterpret_cast<uint32_t*>(r + kRecLenOff)[g] = len[k];
+      reinterpret_cast<uint32_t*>(r + kRecIdOff)[g] = (uint32_t)p;
+    }
   }
 }
 
@@ -714,34 +783,6 @@ __device__ __forceinline__ u32x4 read_landed_slot(uint32_t addr) {
   return v;
 }
 
-// The 8 groups' trailing-byte words, via the scalar unit (a vector load here would
-// make hipcc drain the DMA ring to wait for it).  Lane of group g gets word g.
-__device__ __forceinline__ uint32_t tail_words_scalar(const uint64_t (&a)[8], uint32_t grp) {
-  uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
-  asm volatile(
-      "s_load_dword %0, %8, 0x0\n\t"
-      "s_load_dword %1, %9, 0x0\n\t"
-      "s_load_dword %2, %10, 0x0\n\t"
-      "s_load_dword %3, %11, 0x0\n\t"
-      "s_load_dword %4, %12, 0x0\n\t"
-      "s_load_dword %5, %13, 0x0\n\t"
-      "s_load_dword %6, %14, 0x0\n\t"
-      "s_load_dword %7, %15, 0x0\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&s"(t0), "=&s"(t1), "=&s"(t2), "=&s"(t3), "=&s"(t4), "=&s"(t5), "=&s"(t6), "=&s"(t7)
-      : "s"(a[0]), "s"(a[1]), "s"(a[2]), "s"(a[3]), "s"(a[4]), "s"(a[5]), "s"(a[6]), "s"(a[7])
-      : "memory");
-  uint32_t w = t0;
-  w = grp == 1 ? t1 : w;
-  w = grp == 2 ? t2 : w;
-  w = grp == 3 ? t3 : w;
-  w = grp == 4 ? t4 : w;
-  w = grp == 5 ? t5 : w;
-  w = grp == 6 ? t6 : w;
-  w = grp == 7 ? t7 : w;
-  return w;
-}
-
 // LDS atomic add in asm: hipcc would otherwise order it behind every in-flight LDS-DMA
 // (it cannot tell the counter from the ring) and drain the ring with vmcnt(0).
 __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
@@ -766,7 +807,12 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 // NS > 0: packets of exactly NS steps, the slot loop fully unrolled.  NS == 0: any
 // step count >= kDmaRing (long packets, e.g. 64 KiB buffers: 512 steps), slot loop
 // unrolled by the ring depth.
-template <int NS, bool kTail>
+//
+// Trailing bytes: every packet is run to the next 4-byte boundary (Lx = length
+// rounded up), the z = Lx - length bytes past its end are masked to zero in the last
+// word (lane 0's last slot), and z inverse zero-byte steps after the combine undo
+// them (unshift_zero_bytes).  No separate tail-word load.
+template <int NS>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
@@ -785,8 +831,10 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
     return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
   };
 
-  const PacketGeo g = make_geo(0, u.length);
+  const uint32_t lx = (u.length + 3u) & ~3u, z = lx - u.length;
+  const PacketGeo g = make_geo(0, lx);
   const int32_t ns = NS > 0 ? NS : g.nsteps;
+  const uint32_t last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;  // lane 0 holds the last word
   // This lane's slot-0 chunk relative to its packet's start (> -128: DESIGN.md §3).
   const int64_t rel0 = (int64_t)g.a1 - 16 * (int64_t)(c.k + 1u) - (int64_t)kBytesPerStep * (ns - 1);
   uint32_t am[4], xm[4];
@@ -798,7 +846,6 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   const bool none0 = rel0 <= -16;             // slot-0 chunk wholly before the packet
   const bool part0 = rel0 < 0 && rel0 > -16;  // straddles the packet start
   const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;  // round_meta()'s head field
-  const uint32_t ntail = u.length & 3u;
 
   // Packet of group `grp` in round `rnd`; rounds past the end re-read the last packet.
   auto packet_index = [&](uint64_t rnd, uint32_t grp) -> uint64_t {
@@ -838,16 +885,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
     const uint64_t pb = packet_base(rnd[0]);
     uint64_t pb_next = 0;
     if constexpr (NS == 0) pb_next = packet_base(rnd[1]);
-    uint32_t tw = 0;
-    if constexpr (kTail) {
-      uint64_t ta[8];
-#pragma unroll
-      for (uint32_t gi = 0; gi < 8; ++gi) ta[gi] = u.base + packet_index(rnd[0], gi) * u.stride + g.a1;
-      tw = tail_words_scalar(ta, c.grp);
-    }
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     // One slot: wait for it, refill its LDS slot kDmaRing slots ahead, then the lookups.
-    auto slot = [&](int32_t s, bool top) {
+    auto slot = [&](int32_t s, bool top, bool last) {
       const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
       const int32_t f = s + kDmaRing;
       if constexpr (NS > 0)
@@ -856,11 +896,14 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
         dma(f < ns ? slot_src(pb, f) : slot_src(pb_next, f - ns), q);
       q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
       uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-      if (top) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
+      if (top) {
         const bool below = is_below(pb);
         if (__builtin_amdgcn_ballot_w64(below)) {
           if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
         }
+      }
+      if (last) w3 &= last_mask;  // data only: before the initial-register injection below
+      if (top) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
         h0 = (w0 & am[0]) ^ xm[0];
         h1 = (w1 & am[1]) ^ xm[1];
         h2 = (w2 & am[2]) ^ xm[2];
@@ -875,13 +918,14 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
     };
     if constexpr (NS > 0) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) slot(s, s == 0);
+      for (int s = 0; s < NS; ++s) slot(s, s == 0, s == NS - 1);
     } else {
-      slot(0, true);
-      for (int32_t s = 1; s < ns; ++s) slot(s, false);
+      slot(0, true, false);  // ns >= kDmaRing > 1
+      for (int32_t s = 1; s < ns - 1; ++s) slot(s, false, false);
+      slot(ns - 1, false, true);
     }
     uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
-    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
+    if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     // Lane 8g+j keeps the checksum of group g in this wave's j-th round of 8; one store per 8.
     if (c.k == j) {
@@ -909,12 +953,12 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
 // number of slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the
 // packets with fewer steps read the zero chunk in their leading slots.  Same ring,
 // dispatch and waits as crc32_uniform_dma_kernel, with per-round, per-lane geometry
-// (streaming kernel's round_meta/mask_top/fallback logic).  Three more DMA kinds join
-// the vector-memory stream, each issued at least kDmaRing-1 DMAs before it is read:
-//   - round records (4 B per lane: the 128-B record, lanes 32-63 duplicate it), two
-//     rounds ahead, read with ds_read at the previous round's end;
-//   - the trailing-byte words (4 B per lane, lane 0 of each group), at the round's
-//     start, read at its end.
+// (streaming kernel's round_meta/mask_top/fallback logic).  Round records join the
+// vector-memory stream as one more DMA per round (4 B per lane: the 128-B record,
+// lanes 32-63 duplicate it), issued two rounds ahead and read with ds_read at the
+// previous round's end, at least kDmaRing-1 DMAs later.  Trailing bytes as in the
+// uniform DMA kernel: each packet runs to the next 4-byte boundary with the bytes
+// past its end masked, then unshift_zero_bytes.
 // ---------------------------------------------------------------------------------
 struct RaggedDmaBatch {
   uint64_t base;        // caller's buffer (fallback bound)
@@ -924,11 +968,11 @@ struct RaggedDmaBatch {
 
 struct RaggedRound {
   uint64_t cb;          // this lane's chunk address at slot 0
-  uint64_t tail_addr;   // word holding the trailing bytes, or the zero chunk
   int32_t ns;           // slots of the round (wave-uniform)
   int32_t top_slot;     // slot of this lane's top chunk (ns: packet has no whole word)
-  uint32_t meta;        // round_meta()
+  uint32_t meta;        // round_meta(); the trailing-byte field holds z (bytes run past the end)
   uint32_t id;          // packet id (output index)
+  uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
   bool direct;          // top chunk read directly (not fallback / not before the packet)
 };
 
@@ -945,22 +989,10 @@ __device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint
       : "memory");
 }
 
-__device__ __forceinline__ uint32_t read_lds_word(uint32_t lds_addr) {
-  uint32_t v;
-  asm volatile(
-      "ds_read_b32 %0, %1\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=v"(v)
-      : "v"(lds_addr)
-      : "memory");
-  return v;
-}
-
 __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch b, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
   __shared__ __attribute__((aligned(16))) uint32_t recb[2][kWavesPerBlock][64];
-  __shared__ __attribute__((aligned(16))) uint32_t tailb[kWavesPerBlock][64];
   __shared__ uint32_t next_dispatch;
   constexpr int kLook = 3;
   if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
@@ -992,13 +1024,16 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
       sa = c.base4;
       len = 0;
     }
-    const PacketGeo g = make_geo(sa, len);
+    const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
+    const PacketGeo g = make_geo(sa, len + z);  // runs to the next 4-byte boundary
     RaggedRound rr;
     rr.ns = max(kDmaRing, wave_max_over_groups(g.nsteps));
     rr.cb = g.a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
     rr.top_slot = rr.ns - g.nsteps;
     rr.direct = g.nsteps > 0 && chunk_kind(g, c.k, g.nsteps - 1, c.base4) == kChunkDirect;
-    rr.meta = round_meta(g, c.k, c.base4, valid, rr.tail_addr, c.dummy);
+    uint64_t unused_tail;
+    rr.meta = round_meta(g, c.k, c.base4, valid, unused_tail, c.dummy) | (z << kMetaNTailShift);
+    rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
     rr.id = id;
     return rr;
   };
@@ -1020,14 +1055,12 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
 #pragma unroll
   for (int f = 0; f < kDmaRing; ++f) dma16(unit_src(cur, f), (uint32_t)f);  // cur.ns >= kDmaRing
   const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
-  const uint32_t tail_lds = (uint32_t)(uintptr_t)(LdsVoid*)&tailb[wv][lane];
   uint32_t q = 0;
   uint32_t res = 0, res_id = 0, j = 0;
   bool res_valid = false;
   while (rnd[0] < total_rounds) {
     uint32_t d = 0;
     if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
-    __builtin_amdgcn_global_load_lds((const void*)cur.tail_addr, (LdsVoid*)&tailb[wv][0], 4, 0, 0);
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     for (int32_t s = 0; s < cur.ns; ++s) {
       const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
@@ -1036,11 +1069,12 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
       q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
       uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
       const bool top = s == cur.top_slot;
+      if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
+        if (top && (cur.meta & kMetaFallback))
+          load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
+      }
+      if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
       if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
-        if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
-          if (top && (cur.meta & kMetaFallback))
-            load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
-        }
         if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
       }
       h0 = horner_main(lds, h0, w0, c.lk);
@@ -1049,11 +1083,11 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
       h3 = horner_main(lds, h3, w3, c.lk);
       issue_order_fence();
     }
-    // Round end: the tail word and record rnd[2] have landed (>= kDmaRing-1 DMAs since).
-    const uint32_t tail_word = read_lds_word(tail_lds);
+    // Round end (record rnd[2] has landed: >= kDmaRing-1 DMAs since it was issued).
     uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
-    reg = tail_steps(lds, reg, tail_word, (cur.meta >> kMetaNTailShift) & 3u, (cur.meta >> kMetaTShiftShift) & 3u);
+    const uint32_t z = (cur.meta >> kMetaNTailShift) & 3u;
+    if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
       res = crc;
@@ -1124,25 +1158,36 @@ static unsigned grid_for(uint64_t count, hipError_t& err) {
 }
 
 template <int NS, bool kTail>
-static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks,
-                                   bool dma) {
-  if (dma)
-    hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
-  else
-    hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
+  hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
 
 template <int... I>
 static hipError_t dispatch_uniform(int ns, bool tail, const UniformBatch& u, uint32_t* out, hipStream_t stream,
-                                   unsigned blocks, bool dma, std::integer_sequence<int, I...>) {
+                                   unsigned blocks, std::integer_sequence<int, I...>) {
   hipError_t e = hipErrorInvalidValue;
-  (void)((ns == I + 1 ? (e = tail ? launch_uniform_ns<I + 1, true>(u, out, stream, blocks, dma)
-                            : launch_uniform_ns<I + 1, false>(u, out, stream, blocks, dma),
+  (void)((ns == I + 1 ? (e = tail ? launch_uniform_ns<I + 1, true>(u, out, stream, blocks)
+                            : launch_uniform_ns<I + 1, false>(u, out, stream, blocks),
                    true)
                 : false) ||
    ...);
   return e;
+}
+
+template <int NS>
+static hipError_t launch_uniform_dma(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
+  hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  return hipGetLastError();
+}
+
+// ns in 1..kMaxRoundSteps: the unrolled kernel; longer: the runtime-step kernel (NS = 0).
+template <int... I>
+static hipError_t dispatch_uniform_dma(int ns, const UniformBatch& u, uint32_t* out, hipStream_t stream,
+                                       unsigned blocks, std::integer_sequence<int, I...>) {
+  hipError_t e = hipErrorInvalidValue;
+  const bool hit = ((ns == I + 1 ? (e = launch_uniform_dma<I + 1>(u, out, stream, blocks), true) : false) || ...);
+  return hit ? e : launch_uniform_dma<0>(u, out, stream, blocks);
 }
 
 // ENET_CRC_UNIFORM=regs selects the register-ring uniform kernel (kept for A/B runs).
@@ -1159,25 +1204,17 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   if (count == 0) return hipSuccess;
   hipError_t err;
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
-  const int ns = make_geo(0, length).nsteps;
-  if (((b0 | stride) & 3u) == 0 && ns > kMaxRoundSteps && use_dma_uniform()) {  // long packets
+  if (((b0 | stride) & 3u) == 0 && length > 0 && length <= 0xFFFFFFFCu && use_dma_uniform()) {
+    // One launch covers the whole batch; packets run to the next 4-byte boundary.
+    const int nsx = make_geo(0, (length + 3u) & ~3u).nsteps;
     const unsigned blocks = grid_for(count, err);
     if (err != hipSuccess) return err;
-    const UniformBatch u{b0, stride, length, count};
-    if (length & 3u)
-      hipLaunchKernelGGL((crc32_uniform_dma_kernel<0, true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
-    else
-      hipLaunchKernelGGL((crc32_uniform_dma_kernel<0, false>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
-    return hipGetLastError();
+    return dispatch_uniform_dma(nsx, UniformBatch{b0, stride, length, count}, out, stream, blocks,
+                                std::make_integer_sequence<int, kMaxRoundSteps>{});
   }
+  const int ns = make_geo(0, length).nsteps;
   if (((b0 | stride) & 3u) == 0 && ns >= 1 && ns <= kMaxRoundSteps) {
     const bool tail = (length & 3u) != 0;
-    if (use_dma_uniform()) {  // one launch covers the whole batch
-      const unsigned blocks = grid_for(count, err);
-      if (err != hipSuccess) return err;
-      return dispatch_uniform(ns, tail, UniformBatch{b0, stride, length, count}, out, stream, blocks, true,
-                              std::make_integer_sequence<int, kMaxRoundSteps>{});
-    }
     // Register-ring kernel: packets whose top chunk would begin before `base` (only
     // the first few) go through the streaming kernel, the rest through the uniform one.
     const int64_t off_min = (int64_t)(length & ~3u) - 16 * kLanesPerPacket - (int64_t)kBytesPerStep * (ns - 1);
@@ -1195,7 +1232,7 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
       const unsigned blocks = grid_for(count - p_min, err);
       if (err != hipSuccess) return err;
       const UniformBatch u{b0 + p_min * stride, stride, length, count - p_min};
-      return dispatch_uniform(ns, tail, u, out + p_min, stream, blocks, false,
+      return dispatch_uniform(ns, tail, u, out + p_min, stream, blocks,
                               std::make_integer_sequence<int, kMaxRoundSteps>{});
     }
     return hipSuccess;

@@ -34,6 +34,7 @@ struct OpTables {
   uint32_t sarwate[256];
   uint32_t op[kOpLevels][4][256];
   uint32_t head_k[4];
+  uint8_t inv_top[256];  // inv_top[sarwate[b] >> 24] = b (see m8_inverse)
 };
 
 constexpr uint32_t sarwate_entry(uint32_t b) {
@@ -77,6 +78,7 @@ constexpr OpTables make_op_tables() {
       }
     }
   }
+  for (uint32_t b = 0; b < 256; ++b) t.inv_top[t.sarwate[b] >> 24] = (uint8_t)b;
   uint32_t k = kInitRegister;
   t.head_k[0] = k;
   for (int v = 1; v < 4; ++v) {
@@ -87,5 +89,16 @@ constexpr OpTables make_op_tables() {
 }
 
 inline constexpr OpTables kOpTables = make_op_tables();
+
+constexpr bool top_bytes_are_a_permutation() {
+  bool seen[256] = {};
+  for (uint32_t b = 0; b < 256; ++b) {
+    const uint32_t top = kOpTables.sarwate[b] >> 24;
+    if (seen[top]) return false;
+    seen[top] = true;
+  }
+  return true;
+}
+static_assert(top_bytes_are_a_permutation(), "M8 must be invertible through the table's top bytes");
 
 }  // namespace enet_crc

@@ -3,7 +3,9 @@
 // infrastructure only: it exercises the GF(2) operator tables
 // (rusty_enet_amd/csrc/crc32_ops.hpp), the end-aligned stream decomposition, the
 // head masking / init injection and the fixed-shift combine tree for every lane
-// count the kernel template allows, without a GPU.
+// count the kernel template allows, without a GPU.  kExt models the LDS-DMA kernels'
+// trailing-byte handling: the packet runs to the next 4-byte boundary with the bytes
+// past its end masked to zero, then z inverse zero-byte steps (via inv_top).
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -23,9 +25,17 @@ static const OpTables& T = kOpTables;
 
 static uint32_t op(int lv, uint32_t x) { return apply_op(T.op[lv], x); }
 
-template <int G>
+template <int G, bool kExt = false>
 static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
-  const uint64_t sa = s, ea = s + len, top = sa & ~3ull, a1 = ea & ~3ull;
+  const uint64_t z = kExt && len ? (4 - ((s + len) & 3)) & 3 : 0;
+  const uint64_t sa = s, ea = s + len, top = sa & ~3ull, a1 = kExt ? (ea + z) : (ea & ~3ull);
+  // Word at byte address a (a >= top): the packet's bytes, zeros past its end (kExt).
+  auto word_at = [&](uint64_t a) {
+    uint32_t w = 0;
+    memcpy(&w, buf + a, 4);
+    if (kExt && a + 4 > ea) w &= 0xFFFFFFFFu >> (8 * (a + 4 - ea));
+    return w;
+  };
   const uint64_t nwords = (a1 - top) >> 2;
   constexpr int kMain = __builtin_ctz(4 * G);
   uint32_t reg = kInitRegister;
@@ -38,7 +48,7 @@ static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
       for (int j = 0; j < 4; ++j) {
         const int64_t rel = (int64_t)(a1 - top) - 16 * (c + 1) + 4 * j;
         uint32_t w = 0;
-        if (rel >= 0) memcpy(&w, buf + top + rel, 4);
+        if (rel >= 0) w = word_at(top + rel);
         if (rel == 0) {
           const uint32_t v = (uint32_t)(sa - top);
           w = (w & (0xFFFFFFFFu << (8 * v))) ^ T.head_k[v];
@@ -47,7 +57,7 @@ static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
       }
       for (int64_t i = nsteps - 2; i >= 0; --i) {
         uint32_t q[4];
-        memcpy(q, buf + a1 - 16 * (k + G * i + 1), 16);
+        for (int j = 0; j < 4; ++j) q[j] = word_at(a1 - 16 * (k + G * i + 1) + 4 * j);
         for (int j = 0; j < 4; ++j) h[k][j] = op(kMain, h[k][j]) ^ q[j];
       }
     }
@@ -61,7 +71,14 @@ static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
     }
     reg = op(0, y[0]);
   }
-  for (uint64_t b = (a1 > sa ? a1 : sa); b < ea; ++b) reg = (reg >> 8) ^ T.sarwate[(reg ^ buf[b]) & 0xffu];
+  if constexpr (kExt) {
+    for (uint64_t t = 0; t < z; ++t) {  // M8^-1: the table index from the top byte
+      const uint32_t idx = T.inv_top[reg >> 24];
+      reg = ((reg ^ T.sarwate[idx]) << 8) | idx;
+    }
+  } else {
+    for (uint64_t b = (a1 > sa ? a1 : sa); b < ea; ++b) reg = (reg >> 8) ^ T.sarwate[(reg ^ buf[b]) & 0xffu];
+  }
   return __builtin_bswap32(~reg);
 }
 
@@ -86,8 +103,9 @@ int main() {
     const uint64_t len = it < 6000 ? (uint64_t)(it % 600) : g() % (it % 11 == 0 ? 300000 : 3000);
     if (s + len > buf.size()) continue;
     const uint32_t want = oracle_crc32(buf.data() + s, len);
-    const uint32_t got[4] = {model<2>(buf.data(), s, len), model<4>(buf.data(), s, len),
-                             model<8>(buf.data(), s, len), model<16>(buf.data(), s, len)};
+    const uint32_t got[5] = {model<2>(buf.data(), s, len), model<4>(buf.data(), s, len),
+                             model<8>(buf.data(), s, len), model<16>(buf.data(), s, len),
+                             model<8, true>(buf.data(), s, len)};
     for (uint32_t v : got) {
       if (v != want) {
         if (bad < 10) printf("mismatch s=%llu len=%llu want %08x got %08x\n", (unsigned long long)s,
