@@ -783,6 +783,45 @@ __device__ __forceinline__ u32x4 read_landed_slot(uint32_t addr) {
   return v;
 }
 
+// One Horner step on 4 words fused with the next slot's ring read, so a slot costs one
+// LDS round trip instead of three: the 16 table lookups are issued, then the wait for
+// the next slot's DMA (vmcnt(N)) and its ds_read_b128, then a single lgkmcnt(0) and
+// the XORs.  One asm statement: the compiler never sees a pending LDS result.  The
+// main tables must start at LDS address 0 (checked at the kernel's start).
+template <int N>
+__device__ __forceinline__ void horner_step_and_read(const Lookup& lk, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                                     uint32_t& h3, uint32_t w0, uint32_t w1, uint32_t w2,
+                                                     uint32_t w3, uint32_t next_addr, u32x4& next) {
+  uint32_t a[16];
+  const uint32_t hs[4] = {h0, h1, h2, h3};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[4 * j + t] = __builtin_amdgcn_perm(hs[j], lk.lp, lk.sel[t]);
+  }
+  asm volatile(
+      "ds_read_b32 %5, %5\n\tds_read_b32 %6, %6\n\tds_read_b32 %7, %7\n\tds_read_b32 %8, %8\n\t"
+      "ds_read_b32 %9, %9\n\tds_read_b32 %10, %10\n\tds_read_b32 %11, %11\n\tds_read_b32 %12, %12\n\t"
+      "ds_read_b32 %13, %13\n\tds_read_b32 %14, %14\n\tds_read_b32 %15, %15\n\tds_read_b32 %16, %16\n\t"
+      "ds_read_b32 %17, %17\n\tds_read_b32 %18, %18\n\tds_read_b32 %19, %19\n\tds_read_b32 %20, %20\n\t"
+      "s_waitcnt vmcnt(%26)\n\t"
+      "ds_read_b128 %4, %21\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_bitop3_b32 %5, %5, %6, %7 bitop3:0x96\n\t"
+      "v_bitop3_b32 %0, %5, %8, %22 bitop3:0x96\n\t"
+      "v_bitop3_b32 %9, %9, %10, %11 bitop3:0x96\n\t"
+      "v_bitop3_b32 %1, %9, %12, %23 bitop3:0x96\n\t"
+      "v_bitop3_b32 %13, %13, %14, %15 bitop3:0x96\n\t"
+      "v_bitop3_b32 %2, %13, %16, %24 bitop3:0x96\n\t"
+      "v_bitop3_b32 %17, %17, %18, %19 bitop3:0x96\n\t"
+      "v_bitop3_b32 %3, %17, %20, %25 bitop3:0x96"
+      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(next), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]),
+        "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]),
+        "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
+      : "v"(next_addr), "v"(w0), "v"(w1), "v"(w2), "v"(w3), "i"(N)
+      : "memory");
+}
+
 // LDS atomic add in asm: hipcc would otherwise order it behind every in-flight LDS-DMA
 // (it cannot tell the counter from the ring) and drain the ring with vmcnt(0).
 __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
@@ -868,6 +907,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
 #pragma unroll
   for (int i = 0; i < kLook; ++i) rnd[i] = round_of(wv + (uint32_t)(kWavesPerBlock * i));
   if (rnd[0] >= total_rounds) return;
+  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
 #pragma unroll
   for (int f = 0; f < kDmaRing; ++f) {
     if constexpr (NS > 0)
@@ -875,7 +915,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
     else
       dma(slot_src(packet_base(rnd[0]), f), (uint32_t)f);  // ns >= kDmaRing
   }
-  uint32_t q = 0;  // ring position of the next slot to consume (wave-uniform)
+  uint32_t q = 0;  // ring position of the slot being consumed (wave-uniform)
+  // The ring is read one slot ahead: `nextv` holds the slot about to be consumed.
+  u32x4 nextv = read_landed_slot<kDmaRing - 1>(ring0 + lane * 16u);
   uint32_t res = 0, j = 0;
   uint64_t res_round = 0;
   while (rnd[0] < total_rounds) {
@@ -888,13 +930,14 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     // One slot: wait for it, refill its LDS slot kDmaRing slots ahead, then the lookups.
     auto slot = [&](int32_t s, bool top, bool last) {
-      const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
-      const int32_t f = s + kDmaRing;
+      const u32x4 v = nextv;
+      const int32_t f = s + kDmaRing;  // refill this slot's LDS slot kDmaRing slots ahead
       if constexpr (NS > 0)
         dma(slot_src(packet_base(rnd[f / NS]), f % NS), q);  // f / NS, f % NS fold to constants
       else
         dma(f < ns ? slot_src(pb, f) : slot_src(pb_next, f - ns), q);
       q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
+      const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
       uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
       if (top) {
         const bool below = is_below(pb);
@@ -908,11 +951,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
         h1 = (w1 & am[1]) ^ xm[1];
         h2 = (w2 & am[2]) ^ xm[2];
         h3 = (w3 & am[3]) ^ xm[3];
+        nextv = read_landed_slot<kDmaRing - 1>(next_addr);
       } else {
-        h0 = horner_main(lds, h0, w0, c.lk);
-        h1 = horner_main(lds, h1, w1, c.lk);
-        h2 = horner_main(lds, h2, w2, c.lk);
-        h3 = horner_main(lds, h3, w3, c.lk);
+        horner_step_and_read<kDmaRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, nextv);
       }
       issue_order_fence();  // keep each slot's lookups between its DMA and the next slot's wait
     };
