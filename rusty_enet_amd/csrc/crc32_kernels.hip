@@ -570,8 +570,12 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_hist_kernel(Batch<true
 
 constexpr uint32_t kScanMax = kStepClasses * 1024;  // histogram entries (<= 1024 sort blocks)
 
+// Padded LDS index: thread t scans entries [16t, 16t+16); one pad dword per 32 keeps
+// the 32 threads of a half-wave on distinct banks.
+__device__ __forceinline__ uint32_t scan_slot(uint32_t e) { return e + (e >> 5); }
+
 __global__ __launch_bounds__(1024) void crc32_class_scan_kernel(uint32_t* __restrict__ v, uint32_t n) {
-  __shared__ uint32_t buf[kScanMax];
+  __shared__ uint32_t buf[kScanMax + kScanMax / 32];
   __shared__ uint32_t part[1024];
   uint32_t tmp[kStepClasses];  // coalesced loads, all in flight before the first LDS store
 #pragma unroll
@@ -580,11 +584,12 @@ __global__ __launch_bounds__(1024) void crc32_class_scan_kernel(uint32_t* __rest
     tmp[k] = i < n ? v[i] : 0u;
   }
 #pragma unroll
-  for (uint32_t k = 0; k < kStepClasses; ++k) buf[threadIdx.x + k * 1024] = tmp[k];
+  for (uint32_t k = 0; k < kStepClasses; ++k) buf[scan_slot(threadIdx.x + k * 1024)] = tmp[k];
   __syncthreads();
-  const uint32_t per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+  const uint32_t lo = threadIdx.x * kStepClasses;
   uint32_t sum = 0;
-  for (uint32_t i = lo; i < hi; ++i) sum += buf[i];
+#pragma unroll
+  for (uint32_t i = 0; i < kStepClasses; ++i) sum += buf[scan_slot(lo + i)];
   part[threadIdx.x] = sum;
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the partial sums
@@ -594,13 +599,18 @@ __global__ __launch_bounds__(1024) void crc32_class_scan_kernel(uint32_t* __rest
     __syncthreads();
   }
   uint32_t run = part[threadIdx.x] - sum;
-  for (uint32_t i = lo; i < hi; ++i) {
-    const uint32_t x = buf[i];
-    buf[i] = run;
+#pragma unroll
+  for (uint32_t i = 0; i < kStepClasses; ++i) {
+    const uint32_t x = buf[scan_slot(lo + i)];
+    buf[scan_slot(lo + i)] = run;
     run += x;
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += 1024) v[i] = buf[i];
+#pragma unroll
+  for (uint32_t k = 0; k < kStepClasses; ++k) {
+    const uint32_t i = threadIdx.x + k * 1024;
+    if (i < n) v[i] = buf[scan_slot(i)];
+  }
 }
 
 __global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<true> b, const uint32_t* __restrict__ first,
