@@ -32,16 +32,13 @@
 //   crc32_stream_kernel<U>: any lengths.  A round is padded to a multiple of U
 //     slots and streamed through a U-deep ring; only round boundaries drain.
 //
-// LDS tables (80 KiB):
-//   [0, 64 KiB)   M32^32 tables t = 0..3 (one per register byte), 16 copies each:
-//                 entry i of copy c of table t at dword i*64 + t*16 + c, i.e. bank
-//                 (t&1)*16 + c.  ds_read_b32 serves lanes {0-31} and {32-63} in one
-//                 cycle each when no two lanes of a group hit one bank with different
-//                 addresses; lane l uses copy l%16, and in lookup j the lanes of the
-//                 lower 16 read table j while the upper 16 read table j^1: banks 0-15
-//                 vs 16-31, conflict-free.  Each address is ONE v_perm_b32 with a
-//                 per-lane selector (byte1 = register byte j^half, byte0 = copy/table).
-//   [64 KiB, +)   unreplicated: M32^1 (set 0), tree operators M32^4/8/16 (sets 1..3).
+// LDS tables (76.25 KiB, crc32_layout.hpp has the details):
+//   [0, 64 KiB)   replicated block: one 256-B row per byte value, holding 8 copies of
+//                 the four M32^32 tables (the Horner step) and 8 copies of the four
+//                 M32^1 tables (the in-lane combine).  Lane l reads copy l&7 of table
+//                 j ^ ((l>>3)&3) in lookup j: the 32 lanes of a ds_read_b32 group hit
+//                 32 different banks.  Each address is ONE v_perm_b32.
+//   [64 KiB, +)   unreplicated tree operators M32^4/8/16, then inv_top.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -51,6 +48,7 @@
 
 #include "crc32_geometry.hpp"
 #include "crc32_kernels.hpp"
+#include "crc32_layout.hpp"
 #include "crc32_ops.hpp"
 
 namespace enet_crc {
@@ -75,16 +73,7 @@ typedef __attribute__((address_space(1))) const U32x4A4 GlobalU32x4A4;
 constexpr int kBlock = 1024;
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int G = kLanesPerPacket;
-constexpr uint32_t kMainCopies = 16;
-constexpr uint32_t kMainDwords = 4 * 256 * kMainCopies;  // 4 tables x 256 entries x 16 copies (64 KiB)
-
-constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
-constexpr int kMainLevel = ilog2(4 * G);  // M32^(4G) = M32^32
-constexpr int kTreeLevels = ilog2(G);
-constexpr int kSmallSets = 1 + kTreeLevels;
-constexpr uint32_t kInvTopDword = kMainDwords + kSmallSets * 1024;  // inv_top bytes, 4 per dword
-constexpr uint32_t kLdsDwords = kInvTopDword + 64;
-static_assert(kMainLevel < kOpLevels, "operator level");
+// LDS layout constants, Lookup and make_lookup(): crc32_layout.hpp.
 
 __device__ __forceinline__ uint32_t load_word(uint64_t addr) { return *reinterpret_cast<GlobalU32*>(addr); }
 __device__ __forceinline__ u32x4 load_chunk(uint64_t addr) { return reinterpret_cast<GlobalU32x4A4*>(addr)->v; }
@@ -97,33 +86,24 @@ __device__ __forceinline__ uint32_t lds_at(const uint32_t* lds, uint32_t byte_ad
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
 }
 
-// Per-lane constants of the main-table lookups (see the LDS layout above).
-struct Lookup {
-  uint32_t lp;      // byte j: byte offset of this lane's copy of table t = j ^ half
-  uint32_t sel[4];  // v_perm selectors: byte0 <- lp byte j, byte1 <- h byte (j ^ half)
-};
-
-__device__ __forceinline__ Lookup make_lookup(uint32_t lane) {
-  const uint32_t half = (lane >> 4) & 1u, copy = lane & 15u;
-  Lookup lk;
-  lk.lp = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
-    const uint32_t t = j ^ half;
-    lk.lp |= (copy * 4u + 64u * t) << (8u * j);
-    lk.sel[j] = 0x0C0C0000u | ((4u + t) << 8) | j;
-  }
-  return lk;
+// M(h) ^ w through a replicated set (lp = lk.lp: M32^32, lk.lp1: M32^1): 4 v_perm
+// (each one byte address) + 4 conflict-free ds_read_b32.
+__device__ __forceinline__ uint32_t apply_rep(const uint32_t* lds, uint32_t h, uint32_t w, uint32_t lp,
+                                              const Lookup& lk) {
+  const uint32_t a0 = lookup_addr(h, lp, lk, 0);
+  const uint32_t a1 = lookup_addr(h, lp, lk, 1);
+  const uint32_t a2 = lookup_addr(h, lp, lk, 2);
+  const uint32_t a3 = lookup_addr(h, lp, lk, 3);
+  return xor3(xor3(lds_at(lds, a0), lds_at(lds, a1), lds_at(lds, a2)), lds_at(lds, a3), w);
 }
 
-// h' = M32^32(h) ^ w through the replicated tables: 4 v_perm (each one byte address)
-// + 4 conflict-free ds_read_b32.
+// h' = M32^32(h) ^ w: one Horner step of a word stream.
 __device__ __forceinline__ uint32_t horner_main(const uint32_t* lds, uint32_t h, uint32_t w, const Lookup& lk) {
-  const uint32_t a0 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[0]);
-  const uint32_t a1 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[1]);
-  const uint32_t a2 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[2]);
-  const uint32_t a3 = __builtin_amdgcn_perm(h, lk.lp, lk.sel[3]);
-  return xor3(xor3(lds_at(lds, a0), lds_at(lds, a1), lds_at(lds, a2)), lds_at(lds, a3), w);
+  return apply_rep(lds, h, w, lk.lp, lk);
+}
+
+__device__ __forceinline__ uint32_t sarwate_at(const uint32_t* lds, uint32_t idx) {
+  return lds[idx * kRowDwords + kSarwateDword];
 }
 
 // M32^n(x) through an unreplicated 4x256 table set.
@@ -154,16 +134,18 @@ __device__ __forceinline__ void fill_lds(uint32_t* lds) {
   const int t = threadIdx.x;  // (table, entry) pairs: 4 x 256 = kBlock
   {
     const int tab = t >> 8, i = t & 255;
-    const uint32_t v = g_op_tables.op[kMainLevel][tab][i];
-    const u32x4 vv = {v, v, v, v};
-    u32x4* dst = reinterpret_cast<u32x4*>(lds + i * 64 + tab * 16);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j] = vv;
+    const uint32_t v = g_op_tables.op[kMainLevel][tab][i], v1 = g_op_tables.op[0][tab][i];
+    const u32x4 vv = {v, v, v, v}, vv1 = {v1, v1, v1, v1};
+    u32x4* dst = reinterpret_cast<u32x4*>(lds + i * kRowDwords + tab * kRepCopies);
+    u32x4* dst1 = reinterpret_cast<u32x4*>(lds + i * kRowDwords + kSetM1Bytes / 4 + tab * kRepCopies);
+    dst[0] = vv;
+    dst[1] = vv;
+    dst1[0] = vv1;
+    dst1[1] = vv1;
   }
-  for (int x = t; x < kSmallSets * 1024; x += kBlock) {
-    const int set = x >> 10, rem = x & 1023;
-    const int level = set == 0 ? 0 : set + 1;  // M32^1, then M32^(4*2^(set-1))
-    lds[kMainDwords + x] = g_op_tables.op[level][rem >> 8][rem & 255];
+  for (int x = t; x < kTreeLevels * 1024; x += kBlock) {
+    const int set = x >> 10, rem = x & 1023;  // set l: M32^(4 * 2^l)
+    lds[kTreeDword + x] = g_op_tables.op[set + 2][rem >> 8][rem & 255];
   }
   if (t < 64) {
     const uint8_t* it = g_op_tables.inv_top + 4 * t;
@@ -270,32 +252,30 @@ __device__ __forceinline__ void load_top_words(uint64_t chunk_addr, uint32_t met
 // Combine the 4 word streams of each of the group's 8 lanes into the packet's
 // register (before trailing bytes).  Valid on lane k == 0 of the group.
 __device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
-                                                   uint32_t h3) {
-  const uint32_t* m1 = lds + kMainDwords;
-  uint32_t y = apply_small(m1, h0) ^ h1;
-  y = apply_small(m1, y) ^ h2;
-  y = apply_small(m1, y) ^ h3;
+                                                   uint32_t h3, const Lookup& lk) {
+  // In-lane Horner over the 4 word slots with M32^1 (replicated: conflict-free).
+  uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
+  y = apply_rep(lds, y, h2, lk.lp1, lk);
+  y = apply_rep(lds, y, h3, lk.lp1, lk);
   // Tree levels: only the lanes whose value moves down look it up (the others are
   // masked off, which also keeps them out of the unreplicated tables' bank conflicts).
   const uint32_t k = threadIdx.x & (G - 1);
   uint32_t t = 0;
-  if (k & 1u) t = apply_small(lds + kMainDwords + 1024, y);
+  if (k & 1u) t = apply_small(lds + kTreeDword, y);
   y ^= from_lane_plus<1>(t);
-  if ((k & 3u) == 2u) t = apply_small(lds + kMainDwords + 2048, y);
+  if ((k & 3u) == 2u) t = apply_small(lds + kTreeDword + 1024, y);
   y ^= from_lane_plus<2>(t);
-  if (k == 4u) t = apply_small(lds + kMainDwords + 3072, y);
+  if (k == 4u) t = apply_small(lds + kTreeDword + 2048, y);
   y ^= from_lane_plus<4>(t);
-  if (k == 0u) y = apply_small(m1, y);
-  return y;
+  return apply_rep(lds, y, 0u, lk.lp1, lk);  // every lane (conflict-free); lane k == 0 holds the register
 }
 
 // Sarwate byte steps (src/crc32.rs:43) over `ntail` bytes of `word` from byte `tsh`.
 __device__ __forceinline__ uint32_t tail_steps(const uint32_t* lds, uint32_t reg, uint32_t word, uint32_t ntail,
                                                uint32_t tsh) {
-  const uint32_t* sarwate = lds + kMainDwords + 768;  // M32(b << 24) == CRC table
 #pragma unroll
   for (uint32_t t = 0; t < 3; ++t) {
-    if (t < ntail) reg = (reg >> 8) ^ sarwate[(reg ^ (word >> (8u * (tsh + t)))) & 0xffu];
+    if (t < ntail) reg = (reg >> 8) ^ sarwate_at(lds, (reg ^ (word >> (8u * (tsh + t)))) & 0xffu);
   }
   return reg;
 }
@@ -304,13 +284,12 @@ __device__ __forceinline__ uint32_t tail_steps(const uint32_t* lds, uint32_t reg
 // 4-byte boundary, with the z bytes past its end masked to zero, which leaves
 // M8^z(reg) in the register; M8^-1 recovers the table index from the top byte.
 __device__ __forceinline__ uint32_t unshift_zero_bytes(const uint32_t* lds, uint32_t reg, uint32_t z) {
-  const uint32_t* sarwate = lds + kMainDwords + 768;
   const uint8_t* inv_top = reinterpret_cast<const uint8_t*>(lds + kInvTopDword);
 #pragma unroll
   for (uint32_t t = 0; t < 3; ++t) {
     if (t < z) {
       const uint32_t idx = inv_top[reg >> 24];
-      reg = ((reg ^ sarwate[idx]) << 8) | idx;
+      reg = ((reg ^ sarwate_at(lds, idx)) << 8) | idx;
     }
   }
   return reg;
@@ -318,8 +297,9 @@ __device__ __forceinline__ uint32_t unshift_zero_bytes(const uint32_t* lds, uint
 
 // Round end: combine the 4x8 streams, trailing bytes, store (lane 0 of the group).
 __device__ __forceinline__ void finish_round(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
-                                             uint32_t meta, uint32_t tail_word, uint32_t k, uint32_t* dst) {
-  uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+                                             uint32_t meta, uint32_t tail_word, uint32_t k, const Lookup& lk,
+                                             uint32_t* dst) {
+  uint32_t reg = combine_streams(lds, h0, h1, h2, h3, lk);
   if (meta & kMetaEmpty) reg = kInitRegister;
   reg = tail_steps(lds, reg, tail_word, (meta >> kMetaNTailShift) & 3u, (meta >> kMetaTShiftShift) & 3u);
   if (k == 0 && (meta & kMetaStore)) *dst = __builtin_bswap32(~reg);
@@ -437,7 +417,7 @@ __global__ __launch_bounds__(kBlock) void crc32_rounds_kernel(Batch<kRagged> b, 
       issue_order_fence();
     }
     const uint32_t tw_next = load_word(nxt.tail_addr);
-    finish_round(lds, h0, h1, h2, h3, cur.meta, tw_cur, c.k, out + (first + r * P + c.grp));
+    finish_round(lds, h0, h1, h2, h3, cur.meta, tw_cur, c.k, c.lk, out + (first + r * P + c.grp));
     cur = nxt;
     tw_cur = tw_next;
   }
@@ -508,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
         issue_order_fence();
       }
     }
-    finish_round(lds, h0, h1, h2, h3, meta, tail_word, c.k, out + packet_id(b, p));
+    finish_round(lds, h0, h1, h2, h3, meta, tail_word, c.k, c.lk, out + packet_id(b, p));
   }
 }
 
@@ -743,7 +723,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, u
     }
     uint32_t tw_next = 0;
     if constexpr (kTail) tw_next = load_word(pn - off0 + g.a1);
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
     if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
     const uint64_t p = first + r * P + c.grp;
     if (c.k == 0 && p < u.count) out[p] = __builtin_bswap32(~reg);
@@ -775,8 +755,27 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, u
 // load_top_words only when the chunk would reach below the caller's base.
 // ---------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void LdsVoid;
-constexpr int kDmaRing = 4;                                  // LDS slots per wave
+constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
+constexpr int kRaggedRing = 4;                               // ragged kernel (its round records need LDS too)
 constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
+
+// All LDS of a DMA kernel in ONE variable, tables first: the fused asm lookups use
+// raw LDS addresses and need the tables at address 0 (checked at kernel start).
+template <int R>
+struct UniformDmaLds {
+  uint32_t tables[kLdsDwords];
+  u32x4 ring[R][kWavesPerBlock][64];
+  uint32_t next_dispatch;
+};
+template <int R>
+struct RaggedDmaLds {
+  uint32_t tables[kLdsDwords];
+  u32x4 ring[R][kWavesPerBlock][64];
+  uint32_t recb[2][kWavesPerBlock][64];
+  uint32_t next_dispatch;
+};
+static_assert(sizeof(UniformDmaLds<kUniformRing>) <= 160 * 1024, "LDS");
+static_assert(sizeof(RaggedDmaLds<kRaggedRing>) <= 160 * 1024, "LDS");
 
 // Wait until at most N DMAs are outstanding, read the landed slot (16 B per lane),
 // and wait for the read (the slot is refilled right after).
@@ -807,7 +806,7 @@ __device__ __forceinline__ void horner_step_and_read(const Lookup& lk, uint32_t&
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) a[4 * j + t] = __builtin_amdgcn_perm(hs[j], lk.lp, lk.sel[t]);
+    for (int t = 0; t < 4; ++t) a[4 * j + t] = lookup_addr(hs[j], lk.lp, lk, t);
   }
   asm volatile(
       "ds_read_b32 %5, %5\n\tds_read_b32 %6, %6\n\tds_read_b32 %7, %7\n\tds_read_b32 %8, %8\n\t"
@@ -863,9 +862,11 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 // them (unshift_zero_bytes).  No separate tail-word load.
 template <int NS>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
-  __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
-  __shared__ uint32_t next_dispatch;
+  constexpr int kDmaRing = kUniformRing;
+  __shared__ __attribute__((aligned(16))) UniformDmaLds<kDmaRing> S;
+  uint32_t* const lds = S.tables;
+  auto& ring = S.ring;
+  uint32_t& next_dispatch = S.next_dispatch;
   constexpr int kLook = NS > 0 ? 1 + (NS - 1 + kDmaRing) / NS : 2;  // rounds a wave must know ahead
   if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
   fill_lds(lds);
@@ -975,7 +976,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
       for (int32_t s = 1; s < ns - 1; ++s) slot(s, false, false);
       slot(ns - 1, false, true);
     }
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
     if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     // Lane 8g+j keeps the checksum of group g in this wave's j-th round of 8; one store per 8.
@@ -1041,10 +1042,12 @@ __device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint
 }
 
 __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch b, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
-  __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];
-  __shared__ __attribute__((aligned(16))) uint32_t recb[2][kWavesPerBlock][64];
-  __shared__ uint32_t next_dispatch;
+  constexpr int kDmaRing = kRaggedRing;
+  __shared__ __attribute__((aligned(16))) RaggedDmaLds<kDmaRing> S;
+  uint32_t* const lds = S.tables;
+  auto& ring = S.ring;
+  auto& recb = S.recb;
+  uint32_t& next_dispatch = S.next_dispatch;
   constexpr int kLook = 3;
   if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
   fill_lds(lds);
@@ -1135,7 +1138,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
       issue_order_fence();
     }
     // Round end (record rnd[2] has landed: >= kDmaRing-1 DMAs since it was issued).
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3);
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
     const uint32_t z = (cur.meta >> kMetaNTailShift) & 3u;
     if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);

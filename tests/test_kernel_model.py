@@ -22,3 +22,14 @@ def test_kernel_arithmetic_model(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "bad=0" in out.stdout
+
+
+def test_lds_layout_and_bank_conflicts(tmp_path):
+    """The kernels' replicated-table addressing (crc32_layout.hpp) returns the right
+    operator entries for every lane, and every lookup is bank-conflict-free."""
+    exe = tmp_path / "layout_check"
+    subprocess.check_call(["g++", "-O2", "-std=c++20", "-fconstexpr-ops-limit=200000000",
+                           os.path.join(HERE, "cpp", "layout_check.cpp"), "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad=0 conflicts=0" in out.stdout

@@ -14,6 +14,7 @@ int main(int argc, char** argv) {
   uint8_t* h = (uint8_t*)malloc(n * L);
   uint64_t x = 88172645463325252ull;
   for (uint64_t i = 0; i < n * L; i += 8) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; memcpy(h + i, &x, 8); }
+  if (getenv("ABLATE_CONST")) memset(h, 0x5a, n * L);  // constant bytes (HBM power depends on data)
   hipMemcpy(d, h, n * L, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   for (int i = 0; i < 5; ++i) enet_crc32_uniform_device(d, L, L, n, out, nullptr);
@@ -22,6 +23,10 @@ int main(int argc, char** argv) {
   hipEventRecord(e0, 0);
   for (int i = 0; i < it; ++i) enet_crc32_uniform_device(d, L, L, n, out, nullptr);
   hipEventRecord(e1, 0); hipEventSynchronize(e1);
+  if (hipDeviceSynchronize() != hipSuccess || hipGetLastError() != hipSuccess) {
+    fprintf(stderr, "%s: HIP error, stopping\n", VARIANT_NAME);
+    exit(2);
+  }
   float ms; hipEventElapsedTime(&ms, e0, e1);
   const double us = ms * 1000 / it;
   uint32_t o[4]; hipMemcpy(o, out, 16, hipMemcpyDeviceToHost);

@@ -11,24 +11,27 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void LdsVoid;
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
-constexpr int R = 5, NS = 10;
+constexpr int NS = 10;
 
+template <int R>
 __device__ __forceinline__ u32x4 read_slot(uint32_t a) {
   u32x4 v;
-  asm volatile("s_waitcnt vmcnt(4)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  asm volatile("s_waitcnt vmcnt(%2)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a), "i"(R - 1) : "memory");
   return v;
 }
 
-template <int PAT, int WORK, int NT>
+template <int PAT, int WORK, int NT, int R = 5>
 __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, uint64_t npk, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t tab[20480];
+  constexpr int kTab = R <= 5 ? 20480 : (R == 6 ? 16384 : (R == 7 ? 12288 : 4096));
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kTab];
   __shared__ __attribute__((aligned(16))) u32x4 ring[R][16][64];
-  for (int i = threadIdx.x; i < 20480; i += 1024) tab[i] = i * 2654435761u;
+  for (int i = threadIdx.x; i < kTab; i += 1024) tab[i] = i * 2654435761u;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t g = lane / 8, k = lane % 8;
@@ -40,8 +43,15 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
     const uint64_t rr = wave + (r < nr ? r : nr - 1) * nwaves;  // global round index
     if (PAT == 0) return base + ((uint64_t)(rr * NS + s) % (npk * 1200 / 1024)) * 1024 + lane * 16;
     if (PAT == 3) return base + rr * 9600 + (uint64_t)s * 1024 + lane * 16;
+    if (PAT == 5) {  // 16 lanes per packet: slots 0-4 packets 0-3 of the round, slots 5-9 packets 4-7
+      const uint64_t pk = rr * 8 + (s / 5) * 4 + lane / 16;
+      int64_t off = -80 + 256 * (s % 5) + 16 * (int)(lane % 16);
+      if (off < 0 && pk == 0) off = 0;
+      if (off + 16 > 1200) off = 1200 - 16;
+      return base + pk * 1200 + off;
+    }
     const uint64_t pb = base + (rr * 8 + g) * 1200;
-    int64_t off = (PAT == 1 ? -80 : 0) + 128 * s + 16 * (int)k;
+    int64_t off = (PAT == 1 || PAT == 4 ? -80 : 0) + 128 * s + 16 * (int)(PAT == 4 ? 7 - k : k);
     if (off < 0 && rr * 8 + g == 0) off = 0;
     if (off + 16 > 1200) off = 1200 - 16;
     return pb + off;
@@ -50,13 +60,14 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
     __builtin_amdgcn_global_load_lds((const void*)a, (LdsVoid*)&ring[q][wv][0], 16, 0, NT ? 2 : 0);
   };
   if (nr == 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int f = 0; f < R; ++f) dma(src(f / NS, f % NS), f);
   const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
   uint32_t q = 0, h0 = lane, h1 = lane * 3, h2 = lane * 5, h3 = lane * 7;
   for (uint64_t r = 0; r < nr; ++r) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const u32x4 v = read_slot(ring0 + q * 16384u + lane * 16u);
+      const u32x4 v = read_slot<R>(ring0 + q * 16384u + lane * 16u);
       const int f = s + R;
       dma(src(r + f / NS, f % NS), q);
       q = q + 1 == R ? 0 : q + 1;
@@ -73,24 +84,33 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
   }
   __builtin_amdgcn_s_waitcnt(0);
   out[blockIdx.x * 1024 + threadIdx.x] = h0 ^ h1 ^ h2 ^ h3;
+  if (threadIdx.x == 0) {  // diagnostic clock stamps (own buffer region, never read by the kernel)
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x] = t1 - t0;
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x + 1] = r1 - r0;
+  }
 }
 
-template <int PAT, int WORK, int NT>
+template <int PAT, int WORK, int NT, int R = 5>
 static void run(const char* name, const uint8_t* d, uint64_t npk, uint32_t* out, int blocks) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT, R>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
   CHECK(hipDeviceSynchronize());
   const int iters = 20;
   CHECK(hipEventRecord(e0, 0));
-  for (int w = 0; w < iters; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
+  for (int w = 0; w < iters; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT, R>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
   CHECK(hipEventRecord(e1, 0));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1000.0 / iters;
-  printf("%-44s %8.1f us  %7.1f GB/s\n", name, us, npk * 1200.0 / (us * 1e3));
+  static unsigned long long st[2 * 1024];
+  CHECK(hipMemcpy(st, out + (8 << 20), sizeof(unsigned long long) * 2 * blocks, hipMemcpyDeviceToHost));
+  double ghz = 0;
+  for (int b = 0; b < blocks; ++b) ghz += st[2 * b + 1] ? (double)st[2 * b] / st[2 * b + 1] * 0.1 : 0;
+  printf("%-44s %8.1f us  %7.1f GB/s  clk %.2f GHz\n", name, us, npk * 1200.0 / (us * 1e3), ghz / blocks);
 }
 
 int main() {
@@ -102,7 +122,38 @@ int main() {
   CHECK(hipMalloc(&d, bytes));
   CHECK(hipMalloc(&out, 64 << 20));
   CHECK(hipMemset(d, 0x5a, bytes));
-  printf("CUs=%d, 1M x 1200 B\n", cus);
+  if (getenv("PROBE_RANDOM")) {  // random bytes: HBM/fabric power depends on the data
+    uint8_t* h = (uint8_t*)malloc(bytes);
+    uint64_t x = 88172645463325252ull;
+    for (uint64_t i = 0; i + 8 <= bytes; i += 8) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; memcpy(h + i, &x, 8); }
+    CHECK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
+    free(h);
+  }
+  printf("CUs=%d, 1M x 1200 B, %s data\n", cus, getenv("PROBE_RANDOM") ? "random" : "0x5a");
+  if (getenv("PROBE_RING")) {
+    run<1, 0, 0, 2>("P1 xor R=2", d, npk, out, cus);
+    run<1, 0, 0, 3>("P1 xor R=3", d, npk, out, cus);
+    run<1, 0, 0, 4>("P1 xor R=4", d, npk, out, cus);
+    run<1, 0, 0, 5>("P1 xor R=5", d, npk, out, cus);
+    run<1, 0, 0, 6>("P1 xor R=6", d, npk, out, cus);
+    run<1, 0, 0, 7>("P1 xor R=7", d, npk, out, cus);
+    run<1, 0, 0, 8>("P1 xor R=8", d, npk, out, cus);
+    run<2, 0, 1, 5>("P2 aligned xor nt R=5", d, npk, out, cus);
+    run<2, 0, 1, 8>("P2 aligned xor nt R=8", d, npk, out, cus);
+    run<3, 0, 1, 8>("P3 contiguous xor nt R=8", d, npk, out, cus);
+    run<1, 1, 0, 4>("P1 lookups R=4", d, npk, out, cus);
+    run<1, 1, 0, 6>("P1 lookups R=6", d, npk, out, cus);
+    run<1, 1, 0, 8>("P1 lookups R=8", d, npk, out, cus);
+    run<4, 0, 0, 4>("P4 reversed lanes xor R=4", d, npk, out, cus);
+    run<4, 0, 0, 5>("P4 reversed lanes xor R=5", d, npk, out, cus);
+    run<4, 1, 0, 4>("P4 reversed lanes lookups R=4", d, npk, out, cus);
+    run<5, 0, 0, 4>("P5 16 lanes/packet xor R=4", d, npk, out, cus);
+    run<5, 0, 0, 6>("P5 16 lanes/packet xor R=6", d, npk, out, cus);
+    run<5, 0, 1, 4>("P5 16 lanes/packet xor nt R=4", d, npk, out, cus);
+    run<5, 0, 1, 6>("P5 16 lanes/packet xor nt R=6", d, npk, out, cus);
+    run<1, 0, 1, 6>("P1 xor nt R=6", d, npk, out, cus);
+    return 0;
+  }
   run<0, 0, 0>("P0 global stream, xor", d, npk, out, cus);
   run<1, 0, 0>("P1 crc shape (-80), xor", d, npk, out, cus);
   run<2, 0, 0>("P2 crc shape aligned, xor", d, npk, out, cus);
