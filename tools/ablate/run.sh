@@ -58,6 +58,10 @@ R5D='1:__global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedD
   __shared__ __attribute__((aligned(16))) u32x4 ring[kDmaRing][kWavesPerBlock][64];=>__global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch b, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   __shared__ __attribute__((aligned(16))) u32x4 ring[4][kWavesPerBlock][64];'
+if [ "${ABLATE_SET:-}" = basic ]; then
+  build base
+  ls -la bin; exit 0
+fi
 if [ "${ABLATE_SET:-}" = r5 ]; then
   build base
   build tree2 "$R5A" "$R5B"

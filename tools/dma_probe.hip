@@ -8,6 +8,7 @@
 // work = 0: XOR only; work = 1: 16 table lookups per slot (the kernel's per-slot LDS load).
 //   hipcc --offload-arch=gfx950 -O3 -o tools/dma_probe tools/dma_probe.hip
 #include <hip/hip_runtime.h>
+#include "../rusty_enet_amd/csrc/crc32_layout.hpp"
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -34,6 +35,7 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
   for (int i = threadIdx.x; i < kTab; i += 1024) tab[i] = i * 2654435761u;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const enet_crc::Lookup lk = enet_crc::make_lookup(lane);
   const uint32_t g = lane / 8, k = lane % 8;
   const uint64_t wave = (uint64_t)blockIdx.x * 16 + wv, nwaves = (uint64_t)gridDim.x * 16;
   const uint64_t nrounds_total = npk / 8;
@@ -71,7 +73,13 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
       const int f = s + R;
       dma(src(r + f / NS, f % NS), q);
       q = q + 1 == R ? 0 : q + 1;
-      if (WORK) {
+      if (WORK == 2) {  // the kernel's slot work: 16 conflict-free lookups (crc32_layout.hpp)
+        auto step = [&](uint32_t h, uint32_t w) {
+          return tab[enet_crc::lookup_addr(h, lk.lp, lk, 0) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 1) / 4] ^
+                 tab[enet_crc::lookup_addr(h, lk.lp, lk, 2) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 3) / 4] ^ w;
+        };
+        h0 = step(h0, v.x); h1 = step(h1, v.y); h2 = step(h2, v.z); h3 = step(h3, v.w);
+      } else if (WORK) {
         auto step = [&](uint32_t h, uint32_t w) {
           return tab[h & 0xff] ^ tab[256 + ((h >> 8) & 0xff)] ^ tab[512 + ((h >> 16) & 0xff)] ^ tab[768 + (h >> 24)] ^ w;
         };
@@ -91,16 +99,76 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
   }
 }
 
+
+// Register-staged variant: global_load_dwordx4 straight into a per-round VGPR ring
+// (round r+1's NS chunks load while round r is processed), kernel-like lookups.
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4)));
+template <int NT>
+__global__ __launch_bounds__(1024) void probe_regs(const uint8_t* __restrict__ buf, uint64_t npk, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[16384];
+  for (int i = threadIdx.x; i < 16384; i += 1024) tab[i] = i * 2654435761u;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const enet_crc::Lookup lk = enet_crc::make_lookup(lane);
+  const uint32_t g = lane / 8, k = lane % 8;
+  const uint64_t wave = (uint64_t)blockIdx.x * 16 + wv, nwaves = (uint64_t)gridDim.x * 16;
+  const uint64_t nrounds_total = npk / 8;
+  const uint64_t nr = wave < nrounds_total ? (nrounds_total - wave + nwaves - 1) / nwaves : 0;
+  const uint64_t base = (uint64_t)(uintptr_t)buf;
+  if (nr == 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  typedef __attribute__((address_space(1))) const u32x4a G4;
+  auto src = [&](uint64_t r, int s) -> G4* {
+    const uint64_t rr = wave + (r < nr ? r : nr - 1) * nwaves;
+    const uint64_t pb = base + (rr * 8 + g) * 1200;
+    int64_t off = -80 + 128 * s + 16 * (int)k;
+    if (off < 0 && rr * 8 + g == 0) off = 0;
+    return (G4*)(pb + off);
+  };
+  auto ld = [&](G4* a) -> u32x4a {
+    return NT ? __builtin_nontemporal_load(a) : *a;
+  };
+  u32x4a q[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) { q[s] = ld(src(0, s)); __builtin_amdgcn_sched_barrier(0); }
+  uint32_t h0 = lane, h1 = lane * 3, h2 = lane * 5, h3 = lane * 7;
+  auto step = [&](uint32_t h, uint32_t w) {
+    return tab[enet_crc::lookup_addr(h, lk.lp, lk, 0) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 1) / 4] ^
+           tab[enet_crc::lookup_addr(h, lk.lp, lk, 2) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 3) / 4] ^ w;
+  };
+  for (uint64_t r = 0; r < nr; ++r) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const u32x4a v = q[s];
+      h0 = step(h0, v.x); h1 = step(h1, v.y); h2 = step(h2, v.z); h3 = step(h3, v.w);
+      __builtin_amdgcn_sched_barrier(0);
+      q[s] = ld(src(r + 1, s));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  out[blockIdx.x * 1024 + threadIdx.x] = h0 ^ h1 ^ h2 ^ h3;
+  if (threadIdx.x == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x] = t1 - t0;
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+typedef void (*ProbeFn)(const uint8_t*, uint64_t, uint32_t*);
+static void run_fn(ProbeFn fn, const char* name, const uint8_t* d, uint64_t npk, uint32_t* out, int blocks);
 template <int PAT, int WORK, int NT, int R = 5>
 static void run(const char* name, const uint8_t* d, uint64_t npk, uint32_t* out, int blocks) {
+  run_fn(probe<PAT, WORK, NT, R>, name, d, npk, out, blocks);
+}
+static void run_fn(ProbeFn fn, const char* name, const uint8_t* d, uint64_t npk, uint32_t* out, int blocks) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT, R>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(fn, dim3(blocks), dim3(1024), 0, 0, d, npk, out);
   CHECK(hipDeviceSynchronize());
   const int iters = 20;
   CHECK(hipEventRecord(e0, 0));
-  for (int w = 0; w < iters; ++w) hipLaunchKernelGGL((probe<PAT, WORK, NT, R>), dim3(blocks), dim3(1024), 0, 0, d, npk, out);
+  for (int w = 0; w < iters; ++w) hipLaunchKernelGGL(fn, dim3(blocks), dim3(1024), 0, 0, d, npk, out);
   CHECK(hipEventRecord(e1, 0));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
@@ -130,6 +198,13 @@ int main() {
     free(h);
   }
   printf("CUs=%d, 1M x 1200 B, %s data\n", cus, getenv("PROBE_RANDOM") ? "random" : "0x5a");
+  if (getenv("PROBE_REGS")) {
+    run<1, 0, 0, 5>("P1 xor R=5", d, npk, out, cus);
+    run<1, 2, 0, 5>("P1 kernel lookups, LDS-DMA R=5", d, npk, out, cus);
+    run_fn(probe_regs<0>, "P1 kernel lookups, register ring", d, npk, out, cus);
+    run_fn(probe_regs<1>, "P1 kernel lookups, register ring nt", d, npk, out, cus);
+    return 0;
+  }
   if (getenv("PROBE_RING")) {
     run<1, 0, 0, 2>("P1 xor R=2", d, npk, out, cus);
     run<1, 0, 0, 3>("P1 xor R=3", d, npk, out, cus);
@@ -152,6 +227,8 @@ int main() {
     run<5, 0, 1, 4>("P5 16 lanes/packet xor nt R=4", d, npk, out, cus);
     run<5, 0, 1, 6>("P5 16 lanes/packet xor nt R=6", d, npk, out, cus);
     run<1, 0, 1, 6>("P1 xor nt R=6", d, npk, out, cus);
+    run<1, 2, 0, 4>("P1 kernel lookups R=4", d, npk, out, cus);
+    run<1, 2, 0, 5>("P1 kernel lookups R=5", d, npk, out, cus);
     return 0;
   }
   run<0, 0, 0>("P0 global stream, xor", d, npk, out, cus);
