@@ -6,7 +6,7 @@ CC ?= gcc
 
 LIB := rusty_enet_amd/lib/libenet_crc_amd.so
 ORACLE := oracle/liboracle_crc32.so
-HIP_SRC := rusty_enet_amd/csrc/crc32_kernels.hip rusty_enet_amd/csrc/enet_crc_abi.hip
+HIP_SRC := rusty_enet_amd/csrc/crc32_kernels.hip rusty_enet_amd/csrc/crc32_slot.hip rusty_enet_amd/csrc/enet_crc_abi.hip
 HIP_DEP := $(HIP_SRC) $(wildcard rusty_enet_amd/csrc/*.hpp) include/enet_crc_amd.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -fvisibility=hidden -Wall
 

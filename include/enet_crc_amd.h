@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define ENET_CRC_ABI_VERSION 1
+#define ENET_CRC_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define ENET_CRC_API __attribute__((visibility("default")))
@@ -101,6 +101,48 @@ ENET_CRC_API int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_
  */
 ENET_CRC_API int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t* h_offsets,
                            const uint32_t* h_lengths, uint64_t count, uint32_t* h_out);
+
+/*
+ * Batched receive verify.  Replaces, for `count` received
+ * datagrams, the per-datagram check of src/c/protocol.rs:1470-1502: read the u32 in
+ * the 4-byte checksum slot at d_slot_offsets[p] (header_size - 4, :1470-1478),
+ * overwrite it with d_slot_values[p] (peer.connect_id, or 0 for peer id 4095,
+ * :1483-1492), checksum the datagram (:1493-1499) and accept it when the two match.
+ * Datagram p is d_lengths[p] bytes at d_base + d_offsets[p] (as received, i.e. after
+ * any decompression, :1455-1468).  Outputs: d_crc[p] = the checksum the reference
+ * computes at :1499; d_ok[p] = 1 (accept) or 0 (drop, :1499-1501; also when the slot
+ * does not fit inside the datagram).  The datagram bytes are NOT modified.  The slot
+ * value is applied by linearity after the checksum pass, so the GPU never writes the
+ * buffers.  Device pointers, asynchronous on `hip_stream`.
+ */
+ENET_CRC_API int enet_crc32_verify_ragged_device(const void* d_base, const uint64_t* d_offsets,
+                                                 const uint32_t* d_lengths, const uint32_t* d_slot_offsets,
+                                                 const uint32_t* d_slot_values, uint64_t count, uint32_t* d_crc,
+                                                 uint32_t* d_ok, void* hip_stream);
+
+/*
+ * Batched send insert.  Replaces, for `count` assembled outgoing
+ * datagrams, src/c/protocol.rs:2255-2293: the slot at d_slot_offsets[p] takes
+ * d_slot_values[p] (connect_id, or 0 while outgoing_peer_id >= 4095, :2259-2266),
+ * the datagram is checksummed (:2276-2286) and the checksum is written into the slot
+ * native-endian (:2287-2292).  d_crc[p] receives the checksum too.  Datagrams are
+ * contiguous (header, slot, then the commands) and must not overlap.  A slot that
+ * does not fit inside its datagram is left untouched (d_crc[p] = checksum as stored).
+ */
+ENET_CRC_API int enet_crc32_insert_ragged_device(void* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                                                 const uint32_t* d_slot_offsets, const uint32_t* d_slot_values,
+                                                 uint64_t count, uint32_t* d_crc, void* hip_stream);
+
+/*
+ * Host-side slot correction (no device work; O(log n) table steps).  Given the
+ * checksum `crc` of a datagram whose slot holds `old_slot`, returns the checksum of
+ * the same datagram with the slot holding `new_slot`, where `bytes_after_slot` bytes
+ * follow the slot.  This is what lets a receive loop checksum a whole batch before it
+ * knows each datagram's connect_id: an earlier CONNECT in the same batch can change
+ * it (src/c/protocol.rs:550), and the reference reads it at processing time (:1483).
+ */
+ENET_CRC_API uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, uint32_t new_slot,
+                                             uint32_t bytes_after_slot);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -12,9 +12,13 @@ from .checksum import (  # noqa: F401
     crc32_ragged_device,
     crc32_uniform_device,
     default_context,
+    insert_batch,
+    slot_adjust,
+    verify_batch,
 )
 
 __all__ = [
     "Context", "CrcError", "NativeLibraryMissing", "checksum_fn", "crc32", "crc32_batch",
-    "crc32_ragged_device", "crc32_uniform_device", "default_context",
+    "crc32_ragged_device", "crc32_uniform_device", "default_context", "insert_batch", "slot_adjust",
+    "verify_batch",
 ]

@@ -68,7 +68,15 @@ _SIGNATURES = {
                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     "enet_crc32_ragged_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "enet_crc32_verify_ragged_device": (ctypes.c_int, [ctypes.c_void_p] * 5 + [ctypes.c_uint64] +
+                                        [ctypes.c_void_p] * 3),
+    "enet_crc32_insert_ragged_device": (ctypes.c_int, [ctypes.c_void_p] * 5 + [ctypes.c_uint64] +
+                                        [ctypes.c_void_p] * 2),
+    "enet_crc32_slot_adjust": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32]),
 }
+
+ABI_VERSION = 2
 
 
 def lib() -> ctypes.CDLL:
@@ -88,7 +96,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.restype = restype
             fn.argtypes = argtypes
-        if handle.enet_crc_abi_version() != 1:
+        if handle.enet_crc_abi_version() != ABI_VERSION:
             raise NativeLibraryMissing("ABI version mismatch")
         _lib = handle
     return _lib

@@ -169,3 +169,67 @@ def crc32_batch(data, *, offsets=None, lengths=None, stride: Optional[int] = Non
         out = torch.empty(count, dtype=torch.int32, device=data.device)
     crc32_uniform_device(data.data_ptr(), stride, length, count, out.data_ptr(), sptr)
     return out
+
+
+# checksum slot (SURVEY.md §8(b) batching semantics, §8(f)1-2) ------------------
+
+def slot_adjust(crc: int, old_slot: int, new_slot: int, bytes_after_slot: int) -> int:
+    """Checksum of the same datagram after its 4-byte slot changes old -> new.
+
+    Host-side O(log n) correction (``enet_crc32_slot_adjust``); it transforms a GPU
+    checksum, it never computes one.
+    """
+    return lib().enet_crc32_slot_adjust(crc & 0xFFFFFFFF, old_slot & 0xFFFFFFFF, new_slot & 0xFFFFFFFF,
+                                        int(bytes_after_slot))
+
+
+def _slot_batch_args(data, offsets, lengths, slot_offsets, slot_values):
+    import torch
+
+    if not data.is_cuda or data.dtype != torch.uint8:
+        raise ValueError("data must be a uint8 CUDA/HIP tensor")
+    n = offsets.numel()
+    if offsets.dtype not in (torch.int64, torch.uint64):
+        raise ValueError("offsets must be 64-bit")
+    for name, t in (("lengths", lengths), ("slot_offsets", slot_offsets), ("slot_values", slot_values)):
+        if t.dtype not in (torch.int32, torch.uint32) or t.numel() != n or not t.is_cuda:
+            raise ValueError(f"{name} must be a 32-bit device tensor with one entry per datagram")
+    return n
+
+
+def verify_batch(data, offsets, lengths, slot_offsets, slot_values, stream=None):
+    """Batched receive verify (src/c/protocol.rs:1470-1502 per datagram), device tensors.
+
+    Returns ``(crc, ok)`` int32 tensors: ``crc[p]`` is the checksum the reference
+    computes at :1499 (slot := slot_values[p]), ``ok[p]`` 1 to accept, 0 to drop.
+    ``data`` is not modified.
+    """
+    import torch
+
+    n = _slot_batch_args(data, offsets, lengths, slot_offsets, slot_values)
+    stream = stream or torch.cuda.current_stream(data.device)
+    crc = torch.empty(n, dtype=torch.int32, device=data.device)
+    ok = torch.empty(n, dtype=torch.int32, device=data.device)
+    check(lib().enet_crc32_verify_ragged_device(data.data_ptr(), offsets.data_ptr(), lengths.data_ptr(),
+                                                slot_offsets.data_ptr(), slot_values.data_ptr(), n,
+                                                crc.data_ptr(), ok.data_ptr(), stream.cuda_stream),
+          "enet_crc32_verify_ragged_device")
+    return crc, ok
+
+
+def insert_batch(data, offsets, lengths, slot_offsets, slot_values, stream=None):
+    """Batched send insert (src/c/protocol.rs:2255-2293), in place on device tensors.
+
+    Each datagram's slot takes slot_values[p], the datagram is checksummed and the
+    checksum is written into the slot (native-endian).  Returns the checksums.
+    """
+    import torch
+
+    n = _slot_batch_args(data, offsets, lengths, slot_offsets, slot_values)
+    stream = stream or torch.cuda.current_stream(data.device)
+    crc = torch.empty(n, dtype=torch.int32, device=data.device)
+    check(lib().enet_crc32_insert_ragged_device(data.data_ptr(), offsets.data_ptr(), lengths.data_ptr(),
+                                                slot_offsets.data_ptr(), slot_values.data_ptr(), n,
+                                                crc.data_ptr(), stream.cuda_stream),
+          "enet_crc32_insert_ragged_device")
+    return crc

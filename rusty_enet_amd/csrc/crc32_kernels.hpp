@@ -14,6 +14,15 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
                          uint64_t count, uint32_t* out, hipStream_t stream);
 
+// Slot fix-up after a ragged checksum pass (crc32_slot.hip): crc[p] holds the checksum
+// of datagram p as stored; afterwards the checksum with its 4-byte slot at
+// slot_offsets[p] set to slot_values[p].  insert: that checksum is written into the
+// slot; verify: ok[p] = (it equals the slot's stored u32).  `ladder`: device copy of
+// build_slot_ladder().
+hipError_t launch_slot_fixup(bool insert, uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+                             const uint32_t* slot_offsets, const uint32_t* slot_values, uint64_t count,
+                             uint32_t* crc, uint32_t* ok, const uint32_t* ladder, hipStream_t stream);
+
 // Cached hipDeviceAttributeMultiprocessorCount of the calling thread's device.
 int cu_count_for_current_device();
 

@@ -16,6 +16,7 @@
 
 #include "../../include/enet_crc_amd.h"
 #include "crc32_kernels.hpp"
+#include "crc32_slot.hpp"
 
 namespace enet_crc {
 
@@ -53,6 +54,42 @@ struct DeviceGuard {
 };
 
 }  // namespace
+
+// Operator ladder of the slot correction (crc32_slot.hpp): one host copy, one device
+// copy per device (uploaded on first use, never freed: 128 KiB).
+const uint32_t* host_slot_ladder() {
+  static uint32_t* ladder = [] {
+    uint32_t* l = new uint32_t[kSlotLevels * kSlotLevelDwords];
+    build_slot_ladder(l);
+    return l;
+  }();
+  return ladder;
+}
+
+std::mutex g_ladder_lock;
+uint32_t* g_device_ladder[kMaxDevices];
+
+hipError_t device_slot_ladder(const uint32_t** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(g_ladder_lock);
+  if (!g_device_ladder[dev]) {
+    const size_t bytes = sizeof(uint32_t) * kSlotLevels * kSlotLevelDwords;
+    uint32_t* d = nullptr;
+    e = hipMalloc((void**)&d, bytes);
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(d, host_slot_ladder(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      return e;
+    }
+    g_device_ladder[dev] = d;
+  }
+  *out = g_device_ladder[dev];
+  return hipSuccess;
+}
 
 int cu_count_for_current_device() {
   int dev = 0;
@@ -230,6 +267,43 @@ int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_offsets, cons
   hipError_t e = launch_ragged(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, d_out,
                                static_cast<hipStream_t>(hip_stream));
   return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+}
+
+// Shared body of the batched verify / insert entry points: checksum the datagrams as
+// stored (ragged kernels), then the slot fix-up kernel.
+static int slot_batch(bool insert, uint8_t* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                      const uint32_t* d_slot_offsets, const uint32_t* d_slot_values, uint64_t count, uint32_t* d_crc,
+                      uint32_t* d_ok, void* hip_stream) {
+  if (count == 0) return ENET_CRC_OK;
+  if (!d_base || !d_offsets || !d_lengths || !d_slot_offsets || !d_slot_values || !d_crc || (!insert && !d_ok))
+    return ENET_CRC_E_INVALID;
+  const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  const uint32_t* ladder = nullptr;
+  ENET_HIP_TRY(device_slot_ladder(&ladder));
+  ENET_HIP_TRY(launch_ragged(d_base, d_offsets, d_lengths, count, d_crc, stream));
+  ENET_HIP_TRY(launch_slot_fixup(insert, d_base, d_offsets, d_lengths, d_slot_offsets, d_slot_values, count, d_crc,
+                                 d_ok, ladder, stream));
+  return ENET_CRC_OK;
+}
+
+int enet_crc32_verify_ragged_device(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                                    const uint32_t* d_slot_offsets, const uint32_t* d_slot_values, uint64_t count,
+                                    uint32_t* d_crc, uint32_t* d_ok, void* hip_stream) {
+  // The verify kernel only reads the datagrams (the fix-up kernel is shared with insert).
+  return slot_batch(false, static_cast<uint8_t*>(const_cast<void*>(d_base)), d_offsets, d_lengths, d_slot_offsets,
+                    d_slot_values, count, d_crc, d_ok, hip_stream);
+}
+
+int enet_crc32_insert_ragged_device(void* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                                    const uint32_t* d_slot_offsets, const uint32_t* d_slot_values, uint64_t count,
+                                    uint32_t* d_crc, void* hip_stream) {
+  return slot_batch(true, static_cast<uint8_t*>(d_base), d_offsets, d_lengths, d_slot_offsets, d_slot_values, count,
+                    d_crc, nullptr, hip_stream);
+}
+
+uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, uint32_t new_slot, uint32_t bytes_after_slot) {
+  const uint32_t* l = host_slot_ladder();
+  return crc ^ slot_delta(l, kSlotLevels, l, old_slot ^ new_slot, bytes_after_slot);
 }
 
 int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, uint32_t* out_crc) {

@@ -19,6 +19,8 @@ def test_header_declares_expected_api():
     syms = _declared_symbols()
     assert "enet_crc32_iov" in syms and "enet_crc32_uniform_device" in syms
     assert "enet_crc32_ragged_device" in syms and "enet_crc32_ragged_host" in syms
+    assert "enet_crc32_verify_ragged_device" in syms and "enet_crc32_insert_ragged_device" in syms
+    assert "enet_crc32_slot_adjust" in syms
     assert sorted(_native.exported_symbols()) == syms
 
 
@@ -26,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = _native.lib()
     for name in _declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.enet_crc_abi_version() == 1
+    assert lib.enet_crc_abi_version() == _native.ABI_VERSION == 2
     assert lib.enet_crc_strerror(0) == b"ok"
     assert lib.enet_crc_strerror(_native.ENET_CRC_E_NO_DEVICE) == b"no usable HIP device"
 
@@ -54,3 +56,6 @@ def test_no_device_fails_loudly():
     # device entry points validate arguments before touching the device
     assert lib.enet_crc32_uniform_device(None, 0, 0, 0, None, None) == 0  # empty batch is a no-op
     assert lib.enet_crc32_ragged_device(None, None, None, 5, None, None) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_crc32_verify_ragged_device(None, None, None, None, None, 5, None, None, None) == \
+        _native.ENET_CRC_E_INVALID
+    assert lib.enet_crc32_insert_ragged_device(None, None, None, None, None, 0, None, None) == 0

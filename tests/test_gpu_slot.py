@@ -1,0 +1,213 @@
+"""GPU parity of the batched receive-verify / send-insert paths
+against the oracle restatement of src/c/protocol.rs:1470-1502 (oracle_enet_verify)
+and :2255-2293 (oracle_enet_insert).  Bit-exact: every checksum, every verdict and
+every written slot byte.
+"""
+import numpy as np
+import pytest
+
+import _oracle
+from _data import splitmix64_bytes
+
+torch = pytest.importorskip("torch")
+import rusty_enet_amd as rea  # noqa: E402
+from rusty_enet_amd import protocol  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def oracle_insert(header: bytes, payload: np.ndarray, v: int) -> np.ndarray:
+    hbuf = np.zeros(len(header) + 4, dtype=np.uint8)
+    hbuf[:len(header)] = np.frombuffer(header, dtype=np.uint8)
+    iov = (_oracle.OracleIov * 1)()
+    iov[0].data = payload.ctypes.data if payload.size else None
+    iov[0].len = payload.size
+    _oracle.lib().oracle_enet_insert(hbuf.ctypes.data, len(header), iov, 1, v)
+    return np.concatenate([hbuf, payload])
+
+
+def make_datagrams(seed: int, n: int, max_len: int = 4096):
+    """n ENet-shaped datagrams: header 2 or 4 bytes (+4 slot), random payload, a
+    correct checksum for connect_id v[p]; about a third are then corrupted (a flipped
+    payload/header bit, or verified with a different connect_id)."""
+    rng = np.random.default_rng(seed)
+    grams, hs, vs = [], [], []
+    for p in range(n):
+        hlen = 4 if rng.random() < 0.5 else 2
+        plen = int(rng.integers(0, max_len - hlen - 4 + 1))
+        peer = int(rng.integers(0, 4096))
+        raw = (0x8000 if hlen == 4 else 0) | (int(rng.integers(0, 4)) << 12) | peer
+        header = bytes([raw >> 8, raw & 0xFF]) + (bytes(rng.integers(0, 256, 2, dtype=np.uint8)) if hlen == 4 else b"")
+        v = 0 if peer == 4095 else int(rng.integers(0, 1 << 32, dtype=np.uint64))
+        g = oracle_insert(header, splitmix64_bytes(seed * 1000003 + p, plen), v)
+        kind = rng.integers(0, 3)
+        if kind == 1:
+            g[int(rng.integers(0, g.size))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        elif kind == 2:
+            v ^= 1 << int(rng.integers(0, 32))
+        grams.append(g)
+        hs.append(hlen + 4)
+        vs.append(v)
+    return grams, np.array(hs, dtype=np.uint32), np.array(vs, dtype=np.uint32)
+
+
+def pack(grams, align_gap: int = 0):
+    lens = np.array([g.size for g in grams], dtype=np.uint32)
+    offs = np.zeros(len(grams), dtype=np.uint64)
+    pos = 0
+    for i, g in enumerate(grams):
+        offs[i] = pos
+        pos += g.size + align_gap
+    buf = np.zeros(max(pos, 1), dtype=np.uint8)
+    for i, g in enumerate(grams):
+        buf[int(offs[i]):int(offs[i]) + g.size] = g
+    return buf, offs, lens
+
+
+def oracle_verify(grams, hs, vs):
+    ok, crc = [], []
+    for g, h, v in zip(grams, hs, vs):
+        rx = g.copy()
+        ok.append(_oracle.lib().oracle_enet_verify(rx.ctypes.data, rx.size, int(h), int(v)))
+        crc.append(_oracle.crc32([rx]))  # rx now holds slot := v, as in the reference
+    return np.array(ok, dtype=np.uint32), np.array(crc, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("n,gap", [(1, 0), (257, 0), (3000, 3), (20000, 1)])
+def test_verify_batch_matches_oracle(dev, n, gap):
+    grams, hs, vs = make_datagrams(n + gap, n, max_len=4096 if n <= 3000 else 1400)
+    buf, offs, lens = pack(grams, gap)
+    d = to_dev(buf, dev)
+    crc, ok = rea.verify_batch(d, to_dev(offs.astype(np.int64), dev), to_dev(lens.astype(np.int32), dev),
+                               to_dev((hs - 4).astype(np.int32), dev), to_dev(vs.view(np.int32), dev))
+    torch.cuda.synchronize()
+    want_ok, want_crc = oracle_verify(grams, hs, vs)
+    assert np.array_equal(u32(ok), want_ok)
+    assert np.array_equal(u32(crc), want_crc)
+    assert 0 < want_ok.sum() < n or n == 1
+    assert np.array_equal(d.cpu().numpy(), buf)  # verify never writes the datagrams
+
+
+@pytest.mark.parametrize("n", [1, 300, 5000])
+def test_insert_batch_matches_oracle(dev, n):
+    rng = np.random.default_rng(n)
+    grams, hs, vs, want = [], [], [], []
+    for p in range(n):
+        hlen = int(rng.choice([2, 4]))
+        header = bytes(rng.integers(0, 256, hlen, dtype=np.uint8))
+        payload = splitmix64_bytes(7 * n + p, int(rng.integers(0, 1393)))
+        v = int(rng.integers(0, 1 << 32, dtype=np.uint64))
+        ref = oracle_insert(header, payload, v)
+        g = ref.copy()
+        g[hlen:hlen + 4] = rng.integers(0, 256, 4, dtype=np.uint8)  # garbage in the slot before insert
+        grams.append(g)
+        hs.append(hlen)
+        vs.append(v)
+        want.append(ref)
+    buf, offs, lens = pack(grams, 1)
+    d = to_dev(buf, dev)
+    crc = rea.insert_batch(d, to_dev(offs.astype(np.int64), dev), to_dev(lens.astype(np.int32), dev),
+                           to_dev(np.array(hs, dtype=np.int32), dev),
+                           to_dev(np.array(vs, dtype=np.uint32).view(np.int32), dev))
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    want_buf, _, _ = pack(want, 1)
+    assert np.array_equal(got, want_buf)
+    want_crc = np.array([int.from_bytes(w[h:h + 4].tobytes(), "little") for w, h in zip(want, hs)], dtype=np.uint32)
+    assert np.array_equal(u32(crc), want_crc)
+
+
+def test_golden_enet_datagrams_verify(dev, golden):
+    grams, hs, vs = [], [], []
+    for e in golden["enet"]:
+        grams.append(oracle_insert(bytes.fromhex(e["header_hex"]), splitmix64_bytes(*e["payload"]), e["slot_value"]))
+        assert int.from_bytes(grams[-1][e["header_size"] - 4:e["header_size"]].tobytes(), "little") == e["checksum"]
+        hs.append(e["header_size"])
+        vs.append(e["slot_value"])
+    buf, offs, lens = pack(grams)
+    crc, ok = rea.verify_batch(to_dev(buf, dev), to_dev(offs.astype(np.int64), dev),
+                               to_dev(lens.astype(np.int32), dev), to_dev(np.array(hs, np.int32) - 4, dev),
+                               to_dev(np.array(vs, np.uint32).view(np.int32), dev))
+    assert u32(ok).tolist() == [1] * len(grams)
+    assert u32(crc).tolist() == [e["checksum"] for e in golden["enet"]]
+
+
+def test_slot_edge_cases(dev):
+    """Slot at the very end (0 bytes after it), at offset 0, and slots that do not fit."""
+    base = splitmix64_bytes(99, 64)
+    cases = [(base[:4], 0), (base[:10], 6), (base[:64], 60), (base[:8], 5), (base[:3], 0), (base[:0], 0)]
+    grams = [c[0] for c in cases]
+    so = np.array([c[1] for c in cases], dtype=np.int32)
+    vs = np.array([0x01020304] * len(cases), dtype=np.uint32)
+    buf, offs, lens = pack(grams, 5)
+    crc, ok = rea.verify_batch(to_dev(buf, dev), to_dev(offs.astype(np.int64), dev),
+                               to_dev(lens.astype(np.int32), dev), to_dev(so, dev), to_dev(vs.view(np.int32), dev))
+    got_ok, got_crc = u32(ok), u32(crc)
+    for i, (g, s) in enumerate(cases):
+        if s + 4 <= g.size:
+            rx = g.copy()
+            want = _oracle.lib().oracle_enet_verify(rx.ctypes.data, rx.size, s + 4, int(vs[i]))
+            assert got_ok[i] == want and got_crc[i] == _oracle.crc32([rx]), i
+        else:  # no slot inside the datagram: dropped, checksum as stored
+            assert got_ok[i] == 0 and got_crc[i] == _oracle.crc32([g]), i
+
+
+def test_receive_loop_connect_id_changes_mid_batch(dev):
+    """protocol.verify_received checksums the whole batch in one GPU pass but reads
+    connect_id per datagram, in order, at processing time, like the reference loop
+    (protocol.rs:1652-1692 -> :1483-1487).  Here a CONNECT (peer id 4095) early in the
+    batch makes the host switch peer 7 from connect_id A to B, which decides the
+    verdicts of the later datagrams."""
+    A, B = 0x11111111, 0x22222222
+    plan = [(7, A), (4095, 0), (7, B), (7, A)]  # (peer id, connect_id the sender used)
+    grams = [bytes(oracle_insert(bytes([peer >> 8, peer & 0xFF]), splitmix64_bytes(500 + i, 100 + 37 * i), v))
+             for i, (peer, v) in enumerate(plan)]
+    seen = iter([A, B, B])  # peer 7's connect_id when datagrams 0, 2, 3 are processed
+    calls = []
+
+    def connect_id_of(peer_id):
+        calls.append(peer_id)
+        return next(seen)
+
+    got = protocol.verify_received(grams, connect_id_of)
+    want = []
+    for g, slot_v in zip(grams, [A, 0, B, B]):
+        rx = np.frombuffer(g, dtype=np.uint8).copy()
+        want.append(bool(_oracle.lib().oracle_enet_verify(rx.ctypes.data, rx.size, 6, slot_v)))
+    assert want == [True, True, True, False]
+    assert got == want
+    assert calls == [7, 7, 7]  # never asked for the CONNECT's peer id 4095
+
+
+def test_insert_outgoing_mirror(dev):
+    rng = np.random.default_rng(5)
+    grams, refs, hl, vs = [], [], [], []
+    for i in range(40):
+        h = int(rng.choice([2, 4]))
+        header = bytes(rng.integers(0, 256, h, dtype=np.uint8))
+        payload = splitmix64_bytes(900 + i, int(rng.integers(0, 1400)))
+        v = int(rng.integers(0, 1 << 32, dtype=np.uint64))
+        ref = oracle_insert(header, payload, v)
+        g = bytearray(ref.tobytes())
+        g[h:h + 4] = b"\xff\xff\xff\xff"
+        grams.append(g)
+        refs.append(ref.tobytes())
+        hl.append(h)
+        vs.append(v)
+    crcs = protocol.insert_outgoing(grams, hl, vs)
+    assert [bytes(g) for g in grams] == refs
+    assert crcs == [int.from_bytes(r[h:h + 4], "little") for r, h in zip(refs, hl)]
