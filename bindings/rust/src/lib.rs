@@ -44,6 +44,21 @@ extern "C" {
                                     count: u64, d_out: *mut u32, hip_stream: *mut c_void) -> c_int;
     pub fn enet_crc32_ragged_host(ctx: *mut enet_crc_ctx, h_base: *const c_void, h_offsets: *const u64,
                                   h_lengths: *const u32, count: u64, h_out: *mut u32) -> c_int;
+    pub fn enet_crc32_verify_ragged_device(d_base: *const c_void, d_offsets: *const u64, d_lengths: *const u32,
+                                           d_slot_offsets: *const u32, d_slot_values: *const u32, count: u64,
+                                           d_crc: *mut u32, d_ok: *mut u32, hip_stream: *mut c_void) -> c_int;
+    pub fn enet_crc32_insert_ragged_device(d_base: *mut c_void, d_offsets: *const u64, d_lengths: *const u32,
+                                           d_slot_offsets: *const u32, d_slot_values: *const u32, count: u64,
+                                           d_crc: *mut u32, hip_stream: *mut c_void) -> c_int;
+    pub fn enet_crc32_slot_adjust(crc: u32, old_slot: u32, new_slot: u32, bytes_after_slot: u32) -> u32;
+}
+
+/// Checksum of a datagram after its 4-byte checksum slot changes from `old_slot` to
+/// `new_slot` (`bytes_after_slot` bytes follow the slot).  Host-only; lets a receive
+/// loop checksum a whole batch on the GPU first and apply each datagram's connect_id
+/// when it processes the datagram (rusty_enet src/c/protocol.rs:1483-1499).
+pub fn slot_adjust(crc: u32, old_slot: u32, new_slot: u32, bytes_after_slot: u32) -> u32 {
+    unsafe { enet_crc32_slot_adjust(crc, old_slot, new_slot, bytes_after_slot) }
 }
 
 #[derive(Debug, Clone, Copy, PartialEq, Eq)]
