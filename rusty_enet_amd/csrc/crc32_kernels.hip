@@ -44,6 +44,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <utility>
 
 #include "crc32_geometry.hpp"
@@ -495,13 +496,12 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
 // ---------------------------------------------------------------------------------
 // Ragged batches: order the packets by step count first (a counting sort on device),
 // so the 8 packets of a streaming-kernel round need the same number of slots instead
-// of all being padded to the longest.  Three small kernels, O(12 B) per packet:
+// of all being padded to the longest.  Two small kernels, O(12 B) per packet:
 //   hist:    per-workgroup histogram of step classes over a contiguous packet range,
 //            stored class-major (hist[class * G + block]);
-//   scan:    exclusive scan of that array in place (one workgroup): entry
-//            (class, block) becomes the first output position of that block's packets
-//            of that class;
-//   scatter: same ranges, perm[position] = packet id.
+//   records (or scatter): same ranges; each block first derives its output position
+//            per class from the whole histogram (block_class_bases: the exclusive scan
+//            in class-major order), then writes round records (perm[position] = id).
 // ---------------------------------------------------------------------------------
 constexpr int kStepClasses = 16;  // class = min(nsteps, 15)
 constexpr int kSortBlock = 256;
@@ -517,7 +517,7 @@ __device__ __forceinline__ uint32_t step_class(const Batch<true>& b, uint64_t p)
 
 // The sort kernels give every thread up to kSortPer packets of its block's range;
 // all their descriptors are loaded before any is used (one memory latency, not kSortPer).
-constexpr int kSortPer = 4;
+constexpr int kSortPer = 8;
 
 __device__ __forceinline__ void sort_range(uint64_t count, uint64_t& lo, uint64_t& hi) {
   const uint64_t per = (count + gridDim.x - 1) / gridDim.x;
@@ -548,56 +548,57 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_hist_kernel(Batch<true
   if (threadIdx.x < kStepClasses) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
-constexpr uint32_t kScanMax = kStepClasses * 1024;  // histogram entries (<= 1024 sort blocks)
-
-// Padded LDS index: thread t scans entries [16t, 16t+16); one pad dword per 32 keeps
-// the 32 threads of a half-wave on distinct banks.
-__device__ __forceinline__ uint32_t scan_slot(uint32_t e) { return e + (e >> 5); }
-
-__global__ __launch_bounds__(1024) void crc32_class_scan_kernel(uint32_t* __restrict__ v, uint32_t n) {
-  __shared__ uint32_t buf[kScanMax + kScanMax / 32];
-  __shared__ uint32_t part[1024];
-  uint32_t tmp[kStepClasses];  // coalesced loads, all in flight before the first LDS store
+// First output position of this block's packets of each class, straight from the
+// class-major histogram (no separate scan launch): position(c, b) = sum of all counts of
+// classes < c + counts of class c in blocks < b.  Thread t reads hist[c][t + 256 k]
+// for every class (16 x G/256 loads); the 32 sums (totals, and partials over blocks
+// < blockIdx) are reduced per wave with shuffles and across the 4 waves in LDS.
+__device__ __forceinline__ void block_class_bases(const uint32_t* __restrict__ hist, uint32_t* cur) {
+  __shared__ uint32_t red[kSortBlock / 64][2 * kStepClasses];
+  const uint32_t G = gridDim.x, t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  uint32_t tot[kStepClasses], part[kStepClasses];
 #pragma unroll
-  for (uint32_t k = 0; k < kStepClasses; ++k) {
-    const uint32_t i = threadIdx.x + k * 1024;
-    tmp[k] = i < n ? v[i] : 0u;
+  for (int c = 0; c < kStepClasses; ++c) tot[c] = part[c] = 0;
+  for (uint32_t bb = t; bb < G; bb += kSortBlock) {
+    uint32_t h[kStepClasses];
+#pragma unroll
+    for (int c = 0; c < kStepClasses; ++c) h[c] = hist[c * G + bb];
+#pragma unroll
+    for (int c = 0; c < kStepClasses; ++c) {
+      tot[c] += h[c];
+      part[c] += bb < blockIdx.x ? h[c] : 0u;
+    }
   }
 #pragma unroll
-  for (uint32_t k = 0; k < kStepClasses; ++k) buf[scan_slot(threadIdx.x + k * 1024)] = tmp[k];
+  for (int c = 0; c < kStepClasses; ++c) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      tot[c] += (uint32_t)__shfl_xor((int)tot[c], d, 64);
+      part[c] += (uint32_t)__shfl_xor((int)part[c], d, 64);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < kStepClasses; ++c) {
+      red[w][c] = tot[c];
+      red[w][kStepClasses + c] = part[c];
+    }
+  }
   __syncthreads();
-  const uint32_t lo = threadIdx.x * kStepClasses;
-  uint32_t sum = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kStepClasses; ++i) sum += buf[scan_slot(lo + i)];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the partial sums
-    const uint32_t add = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += add;
-    __syncthreads();
-  }
-  uint32_t run = part[threadIdx.x] - sum;
-#pragma unroll
-  for (uint32_t i = 0; i < kStepClasses; ++i) {
-    const uint32_t x = buf[scan_slot(lo + i)];
-    buf[scan_slot(lo + i)] = run;
-    run += x;
+  if (t < kStepClasses) {
+    uint32_t base = 0;
+    for (uint32_t c = 0; c < t; ++c)
+      for (uint32_t q = 0; q < kSortBlock / 64; ++q) base += red[q][c];
+    for (uint32_t q = 0; q < kSortBlock / 64; ++q) base += red[q][kStepClasses + t];
+    cur[t] = base;
   }
   __syncthreads();
-#pragma unroll
-  for (uint32_t k = 0; k < kStepClasses; ++k) {
-    const uint32_t i = threadIdx.x + k * 1024;
-    if (i < n) v[i] = buf[scan_slot(i)];
-  }
 }
 
-__global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<true> b, const uint32_t* __restrict__ first,
+__global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<true> b, const uint32_t* __restrict__ hist,
                                                                           uint32_t* __restrict__ perm) {
   __shared__ uint32_t cur[kStepClasses];
-  if (threadIdx.x < kStepClasses) cur[threadIdx.x] = first[threadIdx.x * gridDim.x + blockIdx.x];
-  __syncthreads();
+  block_class_bases(hist, cur);
   uint64_t lo, hi;
   sort_range(b.count, lo, hi);
   for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) perm[atomicAdd(&cur[step_class(b, p)], 1u)] = (uint32_t)p;
@@ -609,11 +610,10 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<t
 constexpr uint32_t kRecordBytes = 128;
 constexpr uint32_t kRecLenOff = 64, kRecIdOff = 96;
 
-__global__ __launch_bounds__(kSortBlock) void crc32_class_records_kernel(Batch<true> b, const uint32_t* __restrict__ first,
+__global__ __launch_bounds__(kSortBlock) void crc32_class_records_kernel(Batch<true> b, const uint32_t* __restrict__ hist,
                                                                           uint8_t* __restrict__ recs) {
   __shared__ uint32_t cur[kStepClasses];
-  if (threadIdx.x < kStepClasses) cur[threadIdx.x] = first[threadIdx.x * gridDim.x + blockIdx.x];
-  __syncthreads();
+  block_class_bases(hist, cur);
   uint64_t lo, hi;
   sort_range(b.count, lo, hi);
   for (uint64_t p0 = lo + threadIdx.x; p0 < hi; p0 += kSortBlock * kSortPer) {
@@ -1304,6 +1304,39 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   return L.streaming();
 }
 
+// Stream-ordered scratch for the ragged pre-pass comes from a pool of our own with an
+// unlimited release threshold: freed blocks stay cached, so the per-launch
+// hipMallocFromPoolAsync / hipFreeAsync pair costs no remapping (the default pool,
+// threshold 0, hands memory back at every synchronisation).
+constexpr int kMaxPoolDevices = 64;
+static hipError_t scratch_pool(hipMemPool_t* out) {
+  static std::mutex lock;
+  static hipMemPool_t pools[kMaxPoolDevices];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxPoolDevices) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> g(lock);
+  if (!pools[dev]) {
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t p = nullptr;
+    e = hipMemPoolCreate(&p, &props);
+    if (e != hipSuccess) return e;
+    uint64_t keep = ~0ull;
+    e = hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+    if (e != hipSuccess) {
+      (void)hipMemPoolDestroy(p);
+      return e;
+    }
+    pools[dev] = p;
+  }
+  *out = pools[dev];
+  return hipSuccess;
+}
+
 // Below this many packets the sort costs more than the padding it saves.
 constexpr uint64_t kSortMinPackets = 4096;
 
@@ -1318,25 +1351,28 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // Scratch in stream order: histogram/scan array, then the permutation or the round
+  // Scratch in stream order: histogram, then the permutation or the round
   // records.  ENET_CRC_RAGGED=stream selects the register streaming kernel (A/B runs).
   static const bool stream_kernel = [] {
     const char* v = getenv("ENET_CRC_RAGGED");
     return v && strcmp(v, "stream") == 0;
   }();
-  uint64_t sort_blocks = (count + 4 * kSortBlock - 1) / (4 * kSortBlock);
-  sort_blocks = sort_blocks < 1024 ? sort_blocks : 1024;  // scan: <= 16 entries per thread
+  // >= 4096 packets per sort block: every records/scatter block reads the whole
+  // histogram (16 x sort_blocks entries) to find its output positions.
+  uint64_t sort_blocks = (count + 16 * kSortBlock - 1) / (16 * kSortBlock);
+  sort_blocks = sort_blocks < 1024 ? sort_blocks : 1024;
   const size_t hist_bytes = ((size_t)kStepClasses * sort_blocks * 4 + 255) & ~(size_t)255;
   const uint64_t rounds = (count + kPacketsPerWave - 1) / kPacketsPerWave;
   const size_t tail_bytes = stream_kernel ? (size_t)count * 4 : (size_t)rounds * kRecordBytes;
   void* scratch = nullptr;
-  err = hipMallocAsync(&scratch, hist_bytes + tail_bytes, stream);
+  hipMemPool_t pool = nullptr;
+  err = scratch_pool(&pool);
+  if (err != hipSuccess) return err;
+  err = hipMallocFromPoolAsync(&scratch, hist_bytes + tail_bytes, pool, stream);
   if (err != hipSuccess) return err;
   uint32_t* hist = static_cast<uint32_t*>(scratch);
   uint8_t* second = static_cast<uint8_t*>(scratch) + hist_bytes;
   hipLaunchKernelGGL(crc32_class_hist_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b, hist);
-  hipLaunchKernelGGL(crc32_class_scan_kernel, dim3(1), dim3(1024), 0, stream, hist,
-                     (uint32_t)(kStepClasses * sort_blocks));
   if (stream_kernel) {
     uint32_t* perm = reinterpret_cast<uint32_t*>(second);
     hipLaunchKernelGGL(crc32_class_scatter_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
