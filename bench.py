@@ -158,7 +158,40 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
     return {"value": round(rate, 3), "unit": "GiB/s", "path": "enet_crc32_ragged_host",
             "sample": f"{n} x {L} B from pageable host memory, median of 5 passes",
             "per_call_us": round(per_call_us, 2),
-            "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000"}
+            "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000",
+            "ring": ring_rate(dev, L)}
+
+
+def ring_rate(dev, L: int = 1200, nslots: int = 4, per_slot: int = 40000, rounds: int = 8) -> dict:
+    """Pinned receive ring (enet_crc_ring_*): packets already in pinned slot memory,
+    H2D + kernel + D2H of each slot on its own stream, slots overlapped."""
+    import _oracle
+    from _data import splitmix64_bytes
+    from rusty_enet_amd.ring import ReceiveRing
+
+    with ReceiveRing(dev.index or 0, nslots=nslots, slot_bytes=per_slot * L, slot_packets=per_slot) as ring:
+        for i in range(nslots):
+            data, off, ln, _ = ring.slot(i)
+            data[:] = splitmix64_bytes(ENET_SEED + 200 + i, per_slot * L)
+            off[:] = np.arange(per_slot, dtype=np.uint64) * np.uint64(L)
+            ln[:] = L
+        for i in range(nslots):
+            ring.submit(i, per_slot)
+        for i in range(nslots):
+            ring.wait(i)
+        data, _, _, crcs = ring.slot(0)
+        if not np.array_equal(crcs[:1024], _oracle.crc32_uniform(data[:1024 * L].copy(), L, L, 1024)):
+            raise SystemExit("bench: ring checksums differ from the oracle")
+        t0 = time.perf_counter()
+        for _ in range(rounds):
+            for i in range(nslots):
+                ring.submit(i, per_slot)
+            for i in range(nslots):
+                ring.wait(i)
+        dt = time.perf_counter() - t0
+    return {"value": round(rounds * nslots * per_slot * L / dt / 2**30, 3), "unit": "GiB/s",
+            "path": "enet_crc_ring_submit/wait",
+            "sample": f"{nslots} pinned slots x {per_slot} x {L} B, {rounds} rounds of submit-all/wait-all"}
 
 
 def load_pmc_traffic(config: str):

@@ -144,6 +144,33 @@ ENET_CRC_API int enet_crc32_insert_ragged_device(void* d_base, const uint64_t* d
 ENET_CRC_API uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, uint32_t new_slot,
                                              uint32_t bytes_after_slot);
 
+/*
+ * Pinned receive ring.  The host path above copies pageable
+ * buffers into pinned staging first; a ring lets the receive loop put datagrams
+ * straight into pinned memory (e.g. recvmmsg into slot memory, the role of
+ * host->packet_data in src/c/protocol.rs:1660-1665) and overlaps each slot's
+ * H2D copy, checksum kernel and D2H copy with the other slots'.
+ *
+ * A ring has `nslots` slots on device `device`; each slot owns a pinned byte buffer
+ * of `slot_bytes`, pinned descriptor arrays for `slot_packets` packets (u64 offsets
+ * into the slot's bytes, u32 lengths), a pinned result array, device mirrors and its
+ * own stream.  enet_crc_ring_slot() returns the host pointers (any may be NULL).
+ * enet_crc_ring_submit(ring, i, count) queues H2D -> checksum -> D2H for packets
+ * 0..count-1 of slot i and returns at once; the slot's memory must not be touched
+ * until enet_crc_ring_wait(ring, i) has returned, after which crcs[0..count) hold the
+ * reference checksums.  Submitting a slot that is in flight is ENET_CRC_E_INVALID,
+ * as is a packet outside the slot's bytes.  Calls on one ring are thread-safe.
+ */
+typedef struct enet_crc_ring enet_crc_ring;
+
+ENET_CRC_API int enet_crc_ring_create(int device, uint32_t nslots, uint64_t slot_bytes, uint32_t slot_packets,
+                                      enet_crc_ring** out_ring);
+ENET_CRC_API void enet_crc_ring_destroy(enet_crc_ring* ring);
+ENET_CRC_API int enet_crc_ring_slot(enet_crc_ring* ring, uint32_t slot, uint8_t** data, uint64_t** offsets,
+                                    uint32_t** lengths, uint32_t** crcs);
+ENET_CRC_API int enet_crc_ring_submit(enet_crc_ring* ring, uint32_t slot, uint64_t count);
+ENET_CRC_API int enet_crc_ring_wait(enet_crc_ring* ring, uint32_t slot);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -13,6 +13,7 @@
 #include <atomic>
 #include <mutex>
 #include <new>
+#include <vector>
 
 #include "../../include/enet_crc_amd.h"
 #include "crc32_kernels.hpp"
@@ -129,6 +130,29 @@ struct enet_crc_ctx {
   int device = 0;
   std::mutex lock;
   StageSlot slot[2];
+};
+
+// One slot of a pinned receive ring (include/enet_crc_amd.h).
+struct RingSlot {
+  uint8_t* h_data = nullptr;
+  uint64_t* h_offsets = nullptr;
+  uint32_t* h_lengths = nullptr;
+  uint32_t* h_crcs = nullptr;
+  uint8_t* d_data = nullptr;
+  uint64_t* d_offsets = nullptr;
+  uint32_t* d_lengths = nullptr;
+  uint32_t* d_crcs = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  bool busy = false;
+};
+
+struct enet_crc_ring {
+  int device = 0;
+  uint64_t slot_bytes = 0;
+  uint32_t slot_packets = 0;
+  std::mutex lock;  // guards the busy flags; never held across a device wait
+  std::vector<RingSlot> slots;
 };
 
 namespace {
@@ -394,6 +418,128 @@ int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t
     if (st != ENET_CRC_OK) return st;
   }
   return ENET_CRC_OK;
+}
+
+static void ring_free_slot(RingSlot& s) {
+  if (s.stream) (void)hipStreamSynchronize(s.stream);
+  if (s.h_data) (void)hipHostFree(s.h_data);
+  if (s.h_offsets) (void)hipHostFree(s.h_offsets);
+  if (s.h_lengths) (void)hipHostFree(s.h_lengths);
+  if (s.h_crcs) (void)hipHostFree(s.h_crcs);
+  if (s.d_data) (void)hipFree(s.d_data);
+  if (s.d_offsets) (void)hipFree(s.d_offsets);
+  if (s.d_lengths) (void)hipFree(s.d_lengths);
+  if (s.d_crcs) (void)hipFree(s.d_crcs);
+  if (s.done) (void)hipEventDestroy(s.done);
+  if (s.stream) (void)hipStreamDestroy(s.stream);
+  s = RingSlot{};
+}
+
+int enet_crc_ring_create(int device, uint32_t nslots, uint64_t slot_bytes, uint32_t slot_packets,
+                         enet_crc_ring** out_ring) {
+  if (!out_ring) return ENET_CRC_E_INVALID;
+  *out_ring = nullptr;
+  if (nslots == 0 || nslots > 64 || slot_bytes == 0 || slot_packets == 0) return ENET_CRC_E_INVALID;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return e == hipSuccess ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
+  if (device < 0 || device >= n) return ENET_CRC_E_NO_DEVICE;
+  enet_crc_ring* r = new (std::nothrow) enet_crc_ring();
+  if (!r) return ENET_CRC_E_NOMEM;
+  r->device = device;
+  r->slot_bytes = slot_bytes;
+  r->slot_packets = slot_packets;
+  r->slots.resize(nslots);
+  DeviceGuard g(device);
+  const size_t bytes = (size_t)((slot_bytes + 16 + 15) & ~(uint64_t)15);
+  for (auto& s : r->slots) {
+    hipError_t se = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (se == hipSuccess) se = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (se == hipSuccess) se = hipHostMalloc((void**)&s.h_data, bytes, hipHostMallocDefault);
+    if (se == hipSuccess) se = hipHostMalloc((void**)&s.h_offsets, slot_packets * sizeof(uint64_t), hipHostMallocDefault);
+    if (se == hipSuccess) se = hipHostMalloc((void**)&s.h_lengths, slot_packets * sizeof(uint32_t), hipHostMallocDefault);
+    if (se == hipSuccess) se = hipHostMalloc((void**)&s.h_crcs, slot_packets * sizeof(uint32_t), hipHostMallocDefault);
+    if (se == hipSuccess) se = hipMalloc((void**)&s.d_data, bytes);
+    if (se == hipSuccess) se = hipMalloc((void**)&s.d_offsets, slot_packets * sizeof(uint64_t));
+    if (se == hipSuccess) se = hipMalloc((void**)&s.d_lengths, slot_packets * sizeof(uint32_t));
+    if (se == hipSuccess) se = hipMalloc((void**)&s.d_crcs, slot_packets * sizeof(uint32_t));
+    if (se != hipSuccess) {
+      enet_crc_ring_destroy(r);
+      return fail_hip(se);
+    }
+  }
+  *out_ring = r;
+  return ENET_CRC_OK;
+}
+
+void enet_crc_ring_destroy(enet_crc_ring* r) {
+  if (!r) return;
+  {
+    DeviceGuard g(r->device);
+    for (auto& s : r->slots) ring_free_slot(s);
+  }
+  delete r;
+}
+
+int enet_crc_ring_slot(enet_crc_ring* r, uint32_t slot, uint8_t** data, uint64_t** offsets, uint32_t** lengths,
+                       uint32_t** crcs) {
+  if (!r || slot >= r->slots.size()) return ENET_CRC_E_INVALID;
+  RingSlot& s = r->slots[slot];
+  if (data) *data = s.h_data;
+  if (offsets) *offsets = s.h_offsets;
+  if (lengths) *lengths = s.h_lengths;
+  if (crcs) *crcs = s.h_crcs;
+  return ENET_CRC_OK;
+}
+
+int enet_crc_ring_submit(enet_crc_ring* r, uint32_t slot, uint64_t count) {
+  if (!r || slot >= r->slots.size() || count > r->slot_packets) return ENET_CRC_E_INVALID;
+  RingSlot& s = r->slots[slot];
+  uint64_t span = 0;  // bytes [0, span) of the slot hold every packet
+  for (uint64_t i = 0; i < count; ++i) {
+    const uint64_t o = s.h_offsets[i], l = s.h_lengths[i];
+    if (o > r->slot_bytes || l > r->slot_bytes - o) return ENET_CRC_E_INVALID;
+    span = std::max(span, o + l);
+  }
+  {
+    std::lock_guard<std::mutex> lk(r->lock);
+    if (s.busy) return ENET_CRC_E_INVALID;
+    s.busy = true;
+  }
+  DeviceGuard g(r->device);
+  auto fail = [&](hipError_t e) {
+    std::lock_guard<std::mutex> lk(r->lock);
+    s.busy = false;
+    return fail_hip(e);
+  };
+  hipError_t e = hipSuccess;
+  if (count) {
+    if (span) e = hipMemcpyAsync(s.d_data, s.h_data, span, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(s.d_offsets, s.h_offsets, count * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(s.d_lengths, s.h_lengths, count * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = launch_ragged(s.d_data, s.d_offsets, s.d_lengths, count, s.d_crcs, s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(s.h_crcs, s.d_crcs, count * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream);
+  }
+  if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+  if (e != hipSuccess) return fail(e);
+  return ENET_CRC_OK;
+}
+
+int enet_crc_ring_wait(enet_crc_ring* r, uint32_t slot) {
+  if (!r || slot >= r->slots.size()) return ENET_CRC_E_INVALID;
+  RingSlot& s = r->slots[slot];
+  {
+    std::lock_guard<std::mutex> lk(r->lock);
+    if (!s.busy) return ENET_CRC_OK;
+  }
+  DeviceGuard g(r->device);
+  const hipError_t e = hipEventSynchronize(s.done);
+  std::lock_guard<std::mutex> lk(r->lock);
+  s.busy = false;
+  return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
 }
 
 }  // extern "C"

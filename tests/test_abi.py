@@ -21,6 +21,7 @@ def test_header_declares_expected_api():
     assert "enet_crc32_ragged_device" in syms and "enet_crc32_ragged_host" in syms
     assert "enet_crc32_verify_ragged_device" in syms and "enet_crc32_insert_ragged_device" in syms
     assert "enet_crc32_slot_adjust" in syms
+    assert {"enet_crc_ring_create", "enet_crc_ring_submit", "enet_crc_ring_wait"} <= set(syms)
     assert sorted(_native.exported_symbols()) == syms
 
 
@@ -59,3 +60,8 @@ def test_no_device_fails_loudly():
     assert lib.enet_crc32_verify_ragged_device(None, None, None, None, None, 5, None, None, None) == \
         _native.ENET_CRC_E_INVALID
     assert lib.enet_crc32_insert_ragged_device(None, None, None, None, None, 0, None, None) == 0
+    ring = ctypes.c_void_p()
+    assert lib.enet_crc_ring_create(0, 2, 4096, 16, ctypes.byref(ring)) == _native.ENET_CRC_E_NO_DEVICE
+    assert not ring.value
+    assert lib.enet_crc_ring_create(0, 0, 4096, 16, ctypes.byref(ring)) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_crc_ring_submit(None, 0, 1) == _native.ENET_CRC_E_INVALID
