@@ -640,17 +640,8 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_records_kernel(Batch<t
   }
 }
 
-// ---------------------------------------------------------------------------------
-// Uniform kernel: a uniform batch whose base and stride are multiples of 4, so every
-// packet has the same geometry relative to its own start.  Per-lane chunk offsets,
-// the top-chunk masks and the trailing-byte layout are computed once; a slot costs
-// exactly 4 v_perm + 4 ds_read + 2 v_bitop3 per word, slot offsets ride in the load
-// immediates, and lanes past the end of the batch re-read its last packet (valid
-// memory) without storing.  Contract (host-checked): nsteps(length) == NS, and for
-// every packet of the launch the top chunk starts at or after `lo` (the caller's
-// buffer start): the host routes the first packets that violate it through the
-// streaming kernel.
-// ---------------------------------------------------------------------------------
+// Uniform batches: base and stride multiples of 4, so every packet has the same
+// geometry relative to its own start.
 struct UniformBatch {
   uint64_t base;
   uint64_t stride;
@@ -658,81 +649,8 @@ struct UniformBatch {
   uint64_t count;
 };
 
-template <int NS, bool kTail>
-__global__ __launch_bounds__(kBlock) void crc32_uniform_kernel(UniformBatch u, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
-  fill_lds(lds);
-  __syncthreads();
-  const LaneConsts c = lane_consts(u.base);
-
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-  const uint64_t first = (uint64_t)wave * kPacketsPerWave;
-  const uint64_t P = (uint64_t)gridDim.x * kWavesPerBlock * kPacketsPerWave;
-  if (first >= u.count) return;
-  const uint64_t nrounds = (u.count - first + P - 1) / P;
-
-  // Geometry of a packet starting at offset 0 (the grid word holding sa is at 0).
-  const PacketGeo g = make_geo(0, u.length);
-  const uint64_t off0 = g.a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (NS - 1);  // slot 0
-  const int64_t rel0 = (int64_t)off0;  // slot 0 is every packet's top step
-  // Slot-0 word j: keep if rel0 + 4j >= 0, inject the initial register at rel0 + 4j == 0.
-  uint32_t am[4], xm[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    am[j] = rel0 + 4 * j >= 0 ? 0xFFFFFFFFu : 0u;
-    xm[j] = rel0 + 4 * j == 0 ? kInitRegister : 0u;
-  }
-  const uint32_t ntail = u.length & 3u;
-
-  auto packet_addr = [&](uint64_t r) -> uint64_t {
-    uint64_t p = first + r * P + c.grp;
-    p = p < u.count ? p : u.count - 1;
-    return u.base + p * u.stride;
-  };
-
-  uint64_t pa = packet_addr(0) + off0;
-  u32x4 q[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    q[s] = load_chunk(pa + (uint64_t)kBytesPerStep * s);
-    issue_order_fence();
-  }
-  uint32_t tw = 0;
-  if constexpr (kTail) tw = load_word(pa - off0 + g.a1);
-
-  for (uint64_t r = 0; r < nrounds; ++r) {
-    const uint64_t pn = packet_addr(r + 1) + off0;
-    uint32_t h0, h1, h2, h3;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const u32x4 w = q[s];
-      if (s == 0) {  // top step: M32^32(0) = 0, no lookups; mask to the packet's bytes
-        h0 = (w.x & am[0]) ^ xm[0];
-        h1 = (w.y & am[1]) ^ xm[1];
-        h2 = (w.z & am[2]) ^ xm[2];
-        h3 = (w.w & am[3]) ^ xm[3];
-      } else {
-        h0 = horner_main(lds, h0, w.x, c.lk);
-        h1 = horner_main(lds, h1, w.y, c.lk);
-        h2 = horner_main(lds, h2, w.z, c.lk);
-        h3 = horner_main(lds, h3, w.w, c.lk);
-      }
-      issue_order_fence();
-      q[s] = load_chunk(pn + (uint64_t)kBytesPerStep * s);
-      issue_order_fence();
-    }
-    uint32_t tw_next = 0;
-    if constexpr (kTail) tw_next = load_word(pn - off0 + g.a1);
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
-    if constexpr (kTail) reg = tail_steps(lds, reg, tw, ntail, 0);
-    const uint64_t p = first + r * P + c.grp;
-    if (c.k == 0 && p < u.count) out[p] = __builtin_bswap32(~reg);
-    tw = tw_next;
-  }
-}
-
 // ---------------------------------------------------------------------------------
-// Uniform kernel, LDS-DMA form.  Same arithmetic as crc32_uniform_kernel, but each
+// Uniform kernel, LDS-DMA form.  Same arithmetic as the register kernels, but each
 // slot's 1 KiB (64 lanes x 16 B) arrives through global_load_lds_dwordx4 into a
 // per-wave ring of kDmaRing LDS slots instead of VGPRs:
 //     wait for slot t -> ds_read_b128 -> DMA for slot t + kDmaRing into the same
@@ -1000,6 +918,120 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
 }
 
 // ---------------------------------------------------------------------------------
+// Uniform kernel, register form (ENET_CRC_UNIFORM=regs).  Same geometry, arithmetic,
+// dispatch, result batching and trailing-byte handling as crc32_uniform_dma_kernel,
+// but the packet bytes go straight to VGPRs: the next round's NS chunks are loaded
+// into the ring registers while this round's are consumed (NS KiB per wave in flight)
+// and LDS serves only the table lookups (no DMA write, no ring read).  Every load is
+// unconditional and issued in slot order, so hipcc's waitcnts stay exact.
+// ---------------------------------------------------------------------------------
+struct UniformRegsLds {
+  uint32_t tables[kLdsDwords];
+  uint32_t next_dispatch;
+};
+
+template <int NS>
+__global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) UniformRegsLds S;
+  uint32_t* const lds = S.tables;
+  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(u.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const uint64_t total_rounds = (u.count + kPacketsPerWave - 1) / kPacketsPerWave;
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto round_of = [&](uint32_t d) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
+  const uint32_t lx = (u.length + 3u) & ~3u, z = lx - u.length;
+  const PacketGeo g = make_geo(0, lx);
+  const uint32_t last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+  const int64_t rel0 = (int64_t)g.a1 - 16 * (int64_t)(c.k + 1u) - (int64_t)kBytesPerStep * (NS - 1);
+  uint32_t am[4], xm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    am[j] = rel0 + 4 * j >= 0 ? 0xFFFFFFFFu : 0u;
+    xm[j] = rel0 + 4 * j == 0 ? kInitRegister : 0u;
+  }
+  const bool none0 = rel0 <= -16;
+  const bool part0 = rel0 < 0 && rel0 > -16;
+  const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;
+  auto packet_base = [&](uint64_t rnd) -> uint64_t {
+    const uint64_t p = rnd * kPacketsPerWave + c.grp;
+    return u.base + (p < u.count ? p : u.count - 1) * u.stride;
+  };
+  auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
+  auto slot_src = [&](uint64_t pb, int32_t s) -> uint64_t {
+    if (s != 0) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * s);
+    return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
+  };
+
+  uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
+  if (rnd0 >= total_rounds) return;
+  u32x4 q[NS];
+  {
+    const uint64_t pb = packet_base(rnd0);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      q[s] = load_chunk(slot_src(pb, s));
+      issue_order_fence();
+    }
+  }
+  uint32_t res = 0, j = 0;
+  uint64_t res_round = 0;
+  while (rnd0 < total_rounds) {
+    uint32_t d = 0;
+    if (lane == 0) d = atomicAdd(&S.next_dispatch, 1u);
+    const uint64_t pb = packet_base(rnd0), pbn = packet_base(rnd1);
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint32_t w0 = q[s].x, w1 = q[s].y, w2 = q[s].z, w3 = q[s].w;
+      if (s == 0) {
+        const bool below = is_below(pb);
+        if (__builtin_amdgcn_ballot_w64(below)) {
+          if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
+        }
+      }
+      if (s == NS - 1) w3 &= last_mask;
+      if (s == 0) {
+        h0 = (w0 & am[0]) ^ xm[0];
+        h1 = (w1 & am[1]) ^ xm[1];
+        h2 = (w2 & am[2]) ^ xm[2];
+        h3 = (w3 & am[3]) ^ xm[3];
+      } else {
+        h0 = horner_main(lds, h0, w0, c.lk);
+        h1 = horner_main(lds, h1, w1, c.lk);
+        h2 = horner_main(lds, h2, w2, c.lk);
+        h3 = horner_main(lds, h3, w3, c.lk);
+      }
+      issue_order_fence();
+      q[s] = load_chunk(slot_src(pbn, s));  // the next round's slot s
+      issue_order_fence();
+    }
+    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
+    if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);
+    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    if (c.k == j) {
+      res = crc;
+      res_round = rnd0;
+    }
+    rnd0 = rnd1;
+    rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
+    if (j == 7u || rnd0 >= total_rounds) {
+      const uint64_t p = res_round * kPacketsPerWave + c.grp;
+      if (c.k <= j && p < u.count) out[p] = res;
+      j = 0;
+    } else {
+      ++j;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // Ragged kernel, LDS-DMA form.  Packets come sorted by step class (round records from
 // crc32_class_records_kernel), so the 8 packets of a round need (nearly) the same
 // number of slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the
@@ -1211,22 +1243,10 @@ static unsigned grid_for(uint64_t count, hipError_t& err) {
   return (unsigned)blocks;
 }
 
-template <int NS, bool kTail>
-static hipError_t launch_uniform_ns(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
-  hipLaunchKernelGGL((crc32_uniform_kernel<NS, kTail>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+template <int NS>
+static hipError_t launch_uniform_regs(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
+  hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
-}
-
-template <int... I>
-static hipError_t dispatch_uniform(int ns, bool tail, const UniformBatch& u, uint32_t* out, hipStream_t stream,
-                                   unsigned blocks, std::integer_sequence<int, I...>) {
-  hipError_t e = hipErrorInvalidValue;
-  (void)((ns == I + 1 ? (e = tail ? launch_uniform_ns<I + 1, true>(u, out, stream, blocks)
-                            : launch_uniform_ns<I + 1, false>(u, out, stream, blocks),
-                   true)
-                : false) ||
-   ...);
-  return e;
 }
 
 template <int NS>
@@ -1244,13 +1264,23 @@ static hipError_t dispatch_uniform_dma(int ns, const UniformBatch& u, uint32_t* 
   return hit ? e : launch_uniform_dma<0>(u, out, stream, blocks);
 }
 
-// ENET_CRC_UNIFORM=regs selects the register-ring uniform kernel (kept for A/B runs).
-static bool use_dma_uniform() {
-  static const bool dma = [] {
+// ns in 1..kMaxRoundSteps only (the register ring holds a whole round).
+template <int... I>
+static hipError_t dispatch_uniform_regs(int ns, const UniformBatch& u, uint32_t* out, hipStream_t stream,
+                                        unsigned blocks, std::integer_sequence<int, I...>) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((ns == I + 1 ? (e = launch_uniform_regs<I + 1>(u, out, stream, blocks), true) : false) || ...);
+  return e;
+}
+
+// Aligned uniform batches run the LDS-DMA kernel; ENET_CRC_UNIFORM=regs selects the
+// register-ring kernel instead (packets of up to kMaxRoundSteps steps; A/B runs).
+static bool use_regs_uniform() {
+  static const bool regs = [] {
     const char* v = getenv("ENET_CRC_UNIFORM");
-    return !(v && strcmp(v, "regs") == 0);
+    return v && strcmp(v, "regs") == 0;
   }();
-  return dma;
+  return regs;
 }
 
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
@@ -1258,38 +1288,15 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   if (count == 0) return hipSuccess;
   hipError_t err;
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
-  if (((b0 | stride) & 3u) == 0 && length > 0 && length <= 0xFFFFFFFCu && use_dma_uniform()) {
+  if (((b0 | stride) & 3u) == 0 && length > 0 && length <= 0xFFFFFFFCu) {
     // One launch covers the whole batch; packets run to the next 4-byte boundary.
     const int nsx = make_geo(0, (length + 3u) & ~3u).nsteps;
     const unsigned blocks = grid_for(count, err);
     if (err != hipSuccess) return err;
-    return dispatch_uniform_dma(nsx, UniformBatch{b0, stride, length, count}, out, stream, blocks,
-                                std::make_integer_sequence<int, kMaxRoundSteps>{});
-  }
-  const int ns = make_geo(0, length).nsteps;
-  if (((b0 | stride) & 3u) == 0 && ns >= 1 && ns <= kMaxRoundSteps) {
-    const bool tail = (length & 3u) != 0;
-    // Register-ring kernel: packets whose top chunk would begin before `base` (only
-    // the first few) go through the streaming kernel, the rest through the uniform one.
-    const int64_t off_min = (int64_t)(length & ~3u) - 16 * kLanesPerPacket - (int64_t)kBytesPerStep * (ns - 1);
-    uint64_t p_min = 0;
-    if (off_min < 0) p_min = stride == 0 ? count : ((uint64_t)(-off_min) + stride - 1) / stride;
-    if (p_min > count) p_min = count;
-    if (p_min > 0) {
-      const unsigned blocks = grid_for(p_min, err);
-      if (err != hipSuccess) return err;
-      Launcher<false> L{Batch<false>{b0, nullptr, nullptr, stride, length, p_min}, out, stream, blocks};
-      err = L.streaming();
-      if (err != hipSuccess) return err;
-    }
-    if (p_min < count) {
-      const unsigned blocks = grid_for(count - p_min, err);
-      if (err != hipSuccess) return err;
-      const UniformBatch u{b0 + p_min * stride, stride, length, count - p_min};
-      return dispatch_uniform(ns, tail, u, out + p_min, stream, blocks,
-                              std::make_integer_sequence<int, kMaxRoundSteps>{});
-    }
-    return hipSuccess;
+    const UniformBatch u{b0, stride, length, count};
+    if (use_regs_uniform() && nsx <= kMaxRoundSteps)
+      return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
+    return dispatch_uniform_dma(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
   }
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
