@@ -13,7 +13,8 @@ import os
 import threading
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libenet_crc_amd.so")
+# ENET_CRC_AMD_LIB points at another build of the same library (A/B timing runs).
+LIB_PATH = os.environ.get("ENET_CRC_AMD_LIB") or os.path.join(LIB_DIR, "libenet_crc_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
                            "enet_crc_amd.h")
 
