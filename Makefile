@@ -6,11 +6,12 @@ CC ?= gcc
 
 LIB := rusty_enet_amd/lib/libenet_crc_amd.so
 ORACLE := oracle/liboracle_crc32.so
-HIP_SRC := rusty_enet_amd/csrc/crc32_kernels.hip rusty_enet_amd/csrc/crc32_slot.hip rusty_enet_amd/csrc/enet_crc_abi.hip
-HIP_DEP := $(HIP_SRC) $(wildcard rusty_enet_amd/csrc/*.hpp) include/enet_crc_amd.h
+ORACLE_RANGE := oracle/liboracle_range.so
+HIP_SRC := rusty_enet_amd/csrc/crc32_kernels.hip rusty_enet_amd/csrc/crc32_slot.hip rusty_enet_amd/csrc/enet_crc_abi.hip rusty_enet_amd/csrc/range_coder.hip
+HIP_DEP := $(HIP_SRC) $(wildcard rusty_enet_amd/csrc/*.hpp) include/enet_crc_amd.h include/enet_range_amd.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -fvisibility=hidden -Wall
 
-all: $(LIB) $(ORACLE)
+all: $(LIB) $(ORACLE) $(ORACLE_RANGE)
 
 $(LIB): $(HIP_DEP)
 	mkdir -p $(dir $@)
@@ -20,6 +21,9 @@ $(ORACLE): oracle/crc32_oracle.c
 	$(CC) -O2 -fPIC -shared -pthread -Wall -o $@ $<
 
 clean:
-	rm -f $(LIB) $(ORACLE)
+	rm -f $(LIB) $(ORACLE) $(ORACLE_RANGE)
 
 .PHONY: all clean
+
+$(ORACLE_RANGE): oracle/range_coder_oracle.c
+	$(CC) -O2 -fPIC -shared -Wall -o $@ $<

@@ -15,8 +15,9 @@ import threading
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # ENET_CRC_AMD_LIB points at another build of the same library (A/B timing runs).
 LIB_PATH = os.environ.get("ENET_CRC_AMD_LIB") or os.path.join(LIB_DIR, "libenet_crc_amd.so")
-HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
-                           "enet_crc_amd.h")
+INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADER_PATH = os.path.join(INCLUDE_DIR, "enet_crc_amd.h")
+HEADER_PATHS = [HEADER_PATH, os.path.join(INCLUDE_DIR, "enet_range_amd.h")]
 
 ENET_CRC_OK = 0
 ENET_CRC_E_INVALID = -1
@@ -81,6 +82,12 @@ _SIGNATURES = {
     "enet_crc_ring_slot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_void_p)] * 4),
     "enet_crc_ring_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64]),
     "enet_crc_ring_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    # include/enet_range_amd.h
+    "enet_range_scratch_bytes": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "enet_range_compress_ragged_device": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_uint64] +
+                                          [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_void_p]),
+    "enet_range_decompress_ragged_device": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_uint64] +
+                                            [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_void_p]),
 }
 
 ABI_VERSION = 2

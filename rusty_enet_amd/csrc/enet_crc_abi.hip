@@ -18,6 +18,8 @@
 #include "../../include/enet_crc_amd.h"
 #include "crc32_kernels.hpp"
 #include "crc32_slot.hpp"
+#include "range_coder.hpp"
+#include "../../include/enet_range_amd.h"
 
 namespace enet_crc {
 
@@ -540,6 +542,48 @@ int enet_crc_ring_wait(enet_crc_ring* r, uint32_t slot) {
   std::lock_guard<std::mutex> lk(r->lock);
   s.busy = false;
   return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------
+// Batched range coder (include/enet_range_amd.h; kernels in range_coder.hip).
+
+static int range_batch(bool decompress, const void* d_in, const uint64_t* d_in_offsets,
+                       const uint32_t* d_in_lengths, uint64_t count, void* d_out, const uint64_t* d_out_offsets,
+                       const uint32_t* d_out_limits, uint32_t* d_sizes, void* d_scratch, uint64_t scratch_bytes,
+                       void* hip_stream) {
+  if (count == 0) return ENET_CRC_OK;
+  if (!d_in || !d_in_offsets || !d_in_lengths || !d_out || !d_out_offsets || !d_out_limits || !d_sizes ||
+      !d_scratch || ((uintptr_t)d_scratch & 15) != 0)
+    return ENET_CRC_E_INVALID;
+  const uint64_t workers = scratch_bytes / kRangeArenaBytes;
+  if (workers == 0) return ENET_CRC_E_INVALID;
+  hipError_t e = launch_range(decompress, static_cast<const uint8_t*>(d_in), d_in_offsets, d_in_lengths, count,
+                              static_cast<uint8_t*>(d_out), d_out_offsets, d_out_limits, d_sizes, d_scratch, workers,
+                              static_cast<hipStream_t>(hip_stream));
+  return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+}
+
+extern "C" {
+
+uint64_t enet_range_scratch_bytes(uint64_t workers) { return workers * kRangeArenaBytes; }
+
+int enet_range_compress_ragged_device(const void* d_in, const uint64_t* d_in_offsets, const uint32_t* d_in_lengths,
+                                      uint64_t count, void* d_out, const uint64_t* d_out_offsets,
+                                      const uint32_t* d_out_limits, uint32_t* d_sizes, void* d_scratch,
+                                      uint64_t scratch_bytes, void* hip_stream) {
+  return range_batch(false, d_in, d_in_offsets, d_in_lengths, count, d_out, d_out_offsets, d_out_limits, d_sizes,
+                     d_scratch, scratch_bytes, hip_stream);
+}
+
+int enet_range_decompress_ragged_device(const void* d_in, const uint64_t* d_in_offsets,
+                                        const uint32_t* d_in_lengths, uint64_t count, void* d_out,
+                                        const uint64_t* d_out_offsets, const uint32_t* d_out_limits,
+                                        uint32_t* d_sizes, void* d_scratch, uint64_t scratch_bytes,
+                                        void* hip_stream) {
+  return range_batch(true, d_in, d_in_offsets, d_in_lengths, count, d_out, d_out_offsets, d_out_limits, d_sizes,
+                     d_scratch, scratch_bytes, hip_stream);
 }
 
 }  // extern "C"

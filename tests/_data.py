@@ -37,3 +37,12 @@ def packed_offsets(lengths: np.ndarray) -> np.ndarray:
     if lengths.size > 1:
         np.cumsum(lengths[:-1], dtype=np.uint64, out=off[1:])
     return off
+
+
+def enet_like_bytes(seed: int, n: int) -> np.ndarray:
+    """Compressible game-traffic-like bytes for the range-coder workloads: per byte,
+    ~50 % a small value (0..15), ~25 % zero, ~25 % uniform, from the splitmix64 stream."""
+    r = splitmix64_bytes(seed, 2 * n).reshape(-1, 2) if n else np.zeros((0, 2), np.uint8)
+    sel, v = r[:, 0], r[:, 1]
+    out = np.where(sel < 128, v & np.uint8(15), np.where(sel < 192, np.uint8(0), v))
+    return out.astype(np.uint8)

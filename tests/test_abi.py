@@ -1,4 +1,4 @@
-"""The C-ABI library loads, exports every symbol include/enet_crc_amd.h declares,
+"""The C-ABI library loads, exports every symbol include/*.h declare,
 and fails loudly (negative status, no CPU fallback) when no HIP device exists.
 No compute calls are made here."""
 import ctypes
@@ -10,9 +10,11 @@ from rusty_enet_amd import _native
 
 
 def _declared_symbols():
-    with open(_native.HEADER_PATH) as f:
-        text = f.read()
-    return sorted(set(re.findall(r"ENET_CRC_API\s+[\w\s\*]+?\b(enet_crc\w*)\s*\(", text)))
+    text = ""
+    for path in _native.HEADER_PATHS:
+        with open(path) as f:
+            text += f.read()
+    return sorted(set(re.findall(r"ENET_CRC_API\s+[\w\s\*]+?\b(enet_\w*)\s*\(", text)))
 
 
 def test_header_declares_expected_api():
@@ -22,6 +24,8 @@ def test_header_declares_expected_api():
     assert "enet_crc32_verify_ragged_device" in syms and "enet_crc32_insert_ragged_device" in syms
     assert "enet_crc32_slot_adjust" in syms
     assert {"enet_crc_ring_create", "enet_crc_ring_submit", "enet_crc_ring_wait"} <= set(syms)
+    assert {"enet_range_compress_ragged_device", "enet_range_decompress_ragged_device",
+            "enet_range_scratch_bytes"} <= set(syms)
     assert sorted(_native.exported_symbols()) == syms
 
 
@@ -65,3 +69,10 @@ def test_no_device_fails_loudly():
     assert not ring.value
     assert lib.enet_crc_ring_create(0, 0, 4096, 16, ctypes.byref(ring)) == _native.ENET_CRC_E_INVALID
     assert lib.enet_crc_ring_submit(None, 0, 1) == _native.ENET_CRC_E_INVALID
+    # range coder: argument checks before any device work
+    assert lib.enet_range_scratch_bytes(3) == 3 * 65536
+    args = [None] * 3 + [0] + [None] * 5 + [0, None]
+    assert lib.enet_range_compress_ragged_device(*args) == 0  # empty batch is a no-op
+    args[3] = 4
+    assert lib.enet_range_compress_ragged_device(*args) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_range_decompress_ragged_device(*args) == _native.ENET_CRC_E_INVALID
