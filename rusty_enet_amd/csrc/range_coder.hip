@@ -34,12 +34,12 @@ constexpr uint32_t kTop = 16777216;      // :30
 constexpr uint32_t kArena = 4096;        // :8
 constexpr int kBlock = 256;
 
-// decompress_one is built without optimisation: at -O1 and above the gfx950 build of
-// its body decodes wrong symbols after a few steps, while the host build of the same
-// source is bit-exact (tools/dbg/standalone.hip).  The Model methods it
-// calls stay optimised.
+// Debug hooks: RC_DECODE_ATTR / RC_MODEL_ATTR (e.g. optnone / noinline) for A/B builds.
+// History: an earlier version with byte/short stores into an ENetSymbol struct decoded
+// wrong symbols on gfx950 at -O1 and above (bit-exact at -O0 and on the host); the
+// whole-word layout below is bit-exact optimised (tools/dbg/standalone.hip).
 #ifndef RC_DECODE_ATTR
-#define RC_DECODE_ATTR __attribute__((optnone))
+#define RC_DECODE_ATTR
 #endif
 #ifndef RC_MODEL_ATTR
 #define RC_MODEL_ATTR
@@ -53,19 +53,23 @@ constexpr int kBlock = 256;
 #define RC_FAIL(reason, n) 0u
 #endif
 
-struct alignas(16) Sym {  // ENetSymbol, compress.rs:12-22 (same 16-B layout)
-  uint8_t value;
-  uint8_t count;
-  uint16_t under;
-  uint16_t left;
-  uint16_t right;
-  uint16_t symbols;
-  uint16_t escapes;
-  uint16_t total;
-  uint16_t parent;
-};
+// ENetSymbol (compress.rs:12-22) as four 32-bit words, the same 16 bytes:
+//   x = value | count << 8 | under << 16     y = left | right << 16
+//   z = symbols | escapes << 16              w = total | parent << 16
+// A node is read with one 16-byte load; every update stores whole words rebuilt from
+// the loaded copy (no byte/short stores).
+using Sym = uint4;
 static_assert(sizeof(Sym) == 16, "ENetSymbol is 16 bytes");
 static_assert(kArena * sizeof(Sym) == kRangeArenaBytes, "arena size");
+
+__host__ __device__ inline uint32_t lo16(uint32_t v) { return v & 0xFFFF; }
+__host__ __device__ inline uint32_t hi16(uint32_t v) { return v >> 16; }
+__host__ __device__ inline uint32_t pack(uint32_t lo, uint32_t hi) { return (lo & 0xFFFF) | (hi << 16); }
+__host__ __device__ inline uint32_t sym_value(const Sym& s) { return s.x & 0xFF; }
+__host__ __device__ inline uint32_t sym_count(const Sym& s) { return (s.x >> 8) & 0xFF; }
+__host__ __device__ inline uint32_t sym_x(uint32_t value, uint32_t count, uint32_t under) {
+  return (value & 0xFF) | ((count & 0xFF) << 8) | (under << 16);
+}
 
 struct Model {
   Sym* a;
@@ -74,23 +78,17 @@ struct Model {
   uint32_t order;
 
   __host__ __device__ Sym load(uint32_t i) const { return a[i]; }
+  __host__ __device__ uint32_t* words(uint32_t i) const { return reinterpret_cast<uint32_t*>(a + i); }
 
   RC_MODEL_ATTR __host__ __device__ uint32_t new_symbol(uint32_t value, uint32_t delta) {
     const uint32_t i = next++;
-    Sym s{};
-    s.value = (uint8_t)value;
-    s.count = (uint8_t)delta;
-    s.under = (uint16_t)delta;
-    a[i] = s;
+    a[i] = Sym{sym_x(value, delta, delta), 0u, 0u, 0u};
     return i;
   }
 
   // compress.rs:86-101 / :426-450
   RC_MODEL_ATTR __host__ __device__ void reset() {
-    Sym r{};
-    r.escapes = kEscapeMinimum;
-    r.total = kEscapeMinimum + 256 * kSymbolMinimum;
-    a[0] = r;
+    a[0] = Sym{0u, 0u, pack(0, kEscapeMinimum), pack(kEscapeMinimum + 256 * kSymbolMinimum, 0)};
     next = 1;
     predicted = 0;
     order = 0;
@@ -98,10 +96,12 @@ struct Model {
 
   // `parent` chain target: ~0u = the `predicted` register, else the .parent field of a symbol.
   RC_MODEL_ATTR __host__ __device__ void set_parent(uint32_t slot, uint32_t v) {
-    if (slot == ~0u)
+    if (slot == ~0u) {
       predicted = v;
-    else
-      a[slot].parent = (uint16_t)v;
+    } else {
+      uint32_t* w = words(slot);
+      w[3] = pack(w[3], v);
+    }
   }
 
   // enet_symbol_rescale, compress.rs:42-59, with the left recursion on an explicit
@@ -112,20 +112,21 @@ struct Model {
     uint32_t total = 0;
     for (;;) {
       Sym s = load(i);
-      s.count = (uint8_t)(s.count - (s.count >> 1));
-      a[i].count = s.count;
-      a[i].under = s.count;
-      if (s.left) {  // descend; finish this node after the left subtree returns
+      const uint32_t c0 = sym_count(s);
+      const uint32_t c = c0 - (c0 >> 1);
+      s.x = sym_x(sym_value(s), c, c);
+      words(i)[0] = s.x;
+      if (lo16(s.y)) {  // descend; finish this node after the left subtree returns
         stk[sp++] = i | (total << 16);
-        i += s.left;
+        i += lo16(s.y);
         total = 0;
         continue;
       }
-      total = (total + s.count) & 0xFFFF;
+      total = (total + c) & 0xFFFF;
       // walk right; when a frame ends, return its total to the node that pushed it
       for (;;) {
-        if (s.right) {
-          i += s.right;
+        if (hi16(s.y)) {
+          i += hi16(s.y);
           break;
         }
         if (sp == 0) return total;
@@ -133,77 +134,69 @@ struct Model {
         const uint32_t sub = total;
         i = e & 0xFFFF;
         total = e >> 16;
-        const uint16_t u = (uint16_t)(a[i].under + sub);
-        a[i].under = u;
-        total = (total + u) & 0xFFFF;
         s = load(i);
+        const uint32_t u = (hi16(s.x) + sub) & 0xFFFF;
+        s.x = pack(s.x, u);
+        words(i)[0] = s.x;
+        total = (total + u) & 0xFFFF;
       }
     }
   }
 
   // find-or-insert `value` in context ctx's tree (compress.rs:137-212, :301-376, :847-922).
-  RC_MODEL_ATTR __host__ __device__ uint32_t update(uint32_t ctx, uint32_t value, uint32_t delta, uint32_t& under, uint32_t& count) {
-    const uint32_t first = a[ctx].symbols;
-    if (first == 0) {
+  RC_MODEL_ATTR __host__ __device__ uint32_t update(uint32_t ctx, uint32_t value, uint32_t delta, uint32_t& under,
+                                                    uint32_t& count) {
+    const uint32_t cz = words(ctx)[2];
+    if (lo16(cz) == 0) {
       const uint32_t n = new_symbol(value, delta);
-      a[ctx].symbols = (uint16_t)(n - ctx);
+      words(ctx)[2] = pack(n - ctx, hi16(cz));
       return n;
     }
-    uint32_t i = ctx + first;
+    uint32_t i = ctx + lo16(cz);
     for (;;) {
       const Sym s = load(i);
-      if (value < s.value) {
-        a[i].under = (uint16_t)(s.under + delta);
-        if (s.left) {
-          i += s.left;
+      const uint32_t v = sym_value(s);
+      if (value < v) {
+        words(i)[0] = pack(s.x, hi16(s.x) + delta);
+        if (lo16(s.y)) {
+          i += lo16(s.y);
           continue;
         }
         const uint32_t n = new_symbol(value, delta);
-        a[i].left = (uint16_t)(n - i);
+        words(i)[1] = pack(n - i, hi16(s.y));
         return n;
       }
-      if (value > s.value) {
-        under = (under + s.under) & 0xFFFF;
-        if (s.right) {
-          i += s.right;
+      if (value > v) {
+        under = (under + hi16(s.x)) & 0xFFFF;
+        if (hi16(s.y)) {
+          i += hi16(s.y);
           continue;
         }
         const uint32_t n = new_symbol(value, delta);
-        a[i].right = (uint16_t)(n - i);
+        words(i)[1] = pack(s.y, n - i);
         return n;
       }
-      count = (count + s.count) & 0xFFFF;
-      under = (under + (uint32_t)s.under - s.count) & 0xFFFF;
-      a[i].under = (uint16_t)(s.under + delta);
-      a[i].count = (uint8_t)(s.count + delta);
+      const uint32_t c = sym_count(s), u = hi16(s.x);
+      count = (count + c) & 0xFFFF;
+      under = (under + u - c) & 0xFFFF;
+      words(i)[0] = sym_x(v, c + delta, (u + delta) & 0xFFFF);
       return i;
     }
   }
 
-  // :276-289
-  RC_MODEL_ATTR __host__ __device__ void sub_rescale(uint32_t ctx) {
-    const uint32_t sy = a[ctx].symbols;
-    uint32_t t = sy ? rescale(ctx + sy) : 0;
-    const uint16_t esc = a[ctx].escapes;
-    const uint16_t e2 = (uint16_t)(esc - (esc >> 1));
-    a[ctx].escapes = e2;
-    a[ctx].total = (uint16_t)(t + e2);
-  }
-
-  // :404-419
-  RC_MODEL_ATTR __host__ __device__ void root_rescale() {
-    const uint32_t sy = a[0].symbols;
-    uint32_t t = sy ? rescale(sy) : 0;
-    const uint16_t esc = a[0].escapes;
-    const uint16_t e2 = (uint16_t)(esc - (esc >> 1));
-    a[0].escapes = e2;
-    a[0].total = (uint16_t)(t + e2 + 256 * kSymbolMinimum);
+  // context rescale, :276-289 (root: :404-419, extra = 256 * SYMBOL_MINIMUM)
+  RC_MODEL_ATTR __host__ __device__ void ctx_rescale(uint32_t ctx, uint32_t extra) {
+    const Sym c = load(ctx);
+    const uint32_t t = lo16(c.z) ? rescale(ctx + lo16(c.z)) : 0;
+    const uint32_t e = hi16(c.z) - (hi16(c.z) >> 1);
+    words(ctx)[2] = pack(c.z, e);
+    words(ctx)[3] = pack(t + e + extra, hi16(c.w));
   }
 
   // :421-450, after every symbol
   RC_MODEL_ATTR __host__ __device__ void advance() {
     if (order >= kOrder)
-      predicted = a[predicted].parent;
+      predicted = hi16(words(predicted)[3]);
     else
       ++order;
     if (next >= kArena - kOrder) reset();
@@ -252,8 +245,8 @@ __host__ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t 
       m.set_parent(parent, sym);
       parent = sym;
       const Sym x = m.load(ctx);
-      uint32_t total = x.total;
-      uint32_t esc = x.escapes;
+      uint32_t total = lo16(x.w);
+      uint32_t esc = hi16(x.z);
       if (count > 0) {
         if (!e.put(esc + under, count, total)) return 0;
       } else {
@@ -261,26 +254,27 @@ __host__ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t 
           if (!e.put(0, esc, total)) return 0;
         esc = (esc + kSubEscapeDelta) & 0xFFFF;
         total = (total + kSubEscapeDelta) & 0xFFFF;
-        m.a[ctx].escapes = (uint16_t)esc;
+        m.words(ctx)[2] = pack(x.z, esc);
       }
       total = (total + kSubSymbolDelta) & 0xFFFF;
-      m.a[ctx].total = (uint16_t)total;
-      if (count > 0xff - 2 * kSubSymbolDelta || total > kBottom - 0x100) m.sub_rescale(ctx);
+      m.words(ctx)[3] = pack(total, hi16(x.w));
+      if (count > 0xff - 2 * kSubSymbolDelta || total > kBottom - 0x100) m.ctx_rescale(ctx, 0);
       if (count > 0) {
         coded = true;
         break;
       }
-      ctx = x.parent;
+      ctx = hi16(x.w);
     }
     if (!coded) {  // root, :298-420
       uint32_t under = value * kSymbolMinimum, count = kSymbolMinimum;
       const uint32_t sym = m.update(0, value, kCtxSymbolDelta, under, count);
       m.set_parent(parent, sym);
       const Sym r = m.load(0);
-      if (!e.put((uint32_t)r.escapes + under, count, r.total)) return 0;
-      const uint32_t total = (r.total + kCtxSymbolDelta) & 0xFFFF;
-      m.a[0].total = (uint16_t)total;
-      if (count > 0xff - 2 * kCtxSymbolDelta + kSymbolMinimum || total > kBottom - 0x100) m.root_rescale();
+      if (!e.put(hi16(r.z) + under, count, lo16(r.w))) return 0;
+      const uint32_t total = (lo16(r.w) + kCtxSymbolDelta) & 0xFFFF;
+      m.words(0)[3] = pack(total, hi16(r.w));
+      if (count > 0xff - 2 * kCtxSymbolDelta + kSymbolMinimum || total > kBottom - 0x100)
+        m.ctx_rescale(0, 256 * kSymbolMinimum);
     }
     m.advance();
   }
@@ -314,7 +308,8 @@ struct Decoder {
 };
 
 // enet_range_coder_decompress (compress.rs:463-987).
-RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t out_lim) {
+RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t len, uint8_t* out,
+                                                           uint32_t out_lim) {
   if (len == 0) return 0;  // :481-483
   Decoder d;
   d.in = in;
@@ -329,109 +324,110 @@ RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8
     bool found = false;
     while (ctx != 0) {  // :535-667
       const Sym x = m.load(ctx);
-      if (x.escapes > 0 && x.escapes < x.total) {
-        d.range /= x.total;
+      const uint32_t esc = hi16(x.z), xtotal = lo16(x.w);
+      if (esc > 0 && esc < xtotal) {
+        d.range /= xtotal;
         uint32_t code = ((d.code - d.low) / d.range) & 0xFFFF;
-        if (code < x.escapes) {
-          d.take(0, x.escapes);
+        if (code < esc) {
+          d.take(0, esc);
         } else {
-          code = (code - x.escapes) & 0xFFFF;
+          code = (code - esc) & 0xFFFF;
           uint32_t under = 0, count = 0;
-          if (x.symbols == 0) return RC_FAIL(1, n);
-          uint32_t i = ctx + x.symbols;
+          if (lo16(x.z) == 0) return RC_FAIL(1, n);
+          uint32_t i = ctx + lo16(x.z);
           for (;;) {  // :579-611
             const Sym s = m.load(i);
-            const uint32_t after = (under + s.under) & 0xFFFF;
-            const uint32_t before = s.count;
+            const uint32_t su = hi16(s.x), sc = sym_count(s);
+            const uint32_t after = (under + su) & 0xFFFF;
             if (code >= after) {
-              under = (under + s.under) & 0xFFFF;
-              if (!s.right) return RC_FAIL(2, n);
-              i += s.right;
-            } else if ((int)code < (int)after - (int)before) {
-              m.a[i].under = (uint16_t)(s.under + kSubSymbolDelta);
-              if (!s.left) return RC_FAIL(3, n);
-              i += s.left;
+              under = after;
+              if (!hi16(s.y)) return RC_FAIL(2, n);
+              i += hi16(s.y);
+            } else if ((int)code < (int)after - (int)sc) {
+              m.words(i)[0] = pack(s.x, su + kSubSymbolDelta);
+              if (!lo16(s.y)) return RC_FAIL(3, n);
+              i += lo16(s.y);
             } else {
-              value = s.value;
-              count = (count + s.count) & 0xFFFF;
-              under = (after - before) & 0xFFFF;
-              m.a[i].under = (uint16_t)(s.under + kSubSymbolDelta);
-              m.a[i].count = (uint8_t)(s.count + kSubSymbolDelta);
+              value = sym_value(s);
+              count = (count + sc) & 0xFFFF;
+              under = (after - sc) & 0xFFFF;
+              m.words(i)[0] = sym_x(value, sc + kSubSymbolDelta, (su + kSubSymbolDelta) & 0xFFFF);
               break;
             }
           }
           bottom = i;
-          d.take((uint32_t)x.escapes + under, count);
-          const uint32_t total = (x.total + kSubSymbolDelta) & 0xFFFF;
-          m.a[ctx].total = (uint16_t)total;
-          if (count > 0xff - 2 * kSubSymbolDelta || total > kBottom - 0x100) m.sub_rescale(ctx);
+          d.take(esc + under, count);
+          const uint32_t total = (xtotal + kSubSymbolDelta) & 0xFFFF;
+          m.words(ctx)[3] = pack(total, hi16(x.w));
+          if (count > 0xff - 2 * kSubSymbolDelta || total > kBottom - 0x100) m.ctx_rescale(ctx, 0);
           found = true;
           break;
         }
       }
-      ctx = x.parent;
+      ctx = hi16(x.w);
     }
     if (!found) {  // root, :668-840
       const Sym r = m.load(0);
-      d.range /= r.total;
+      d.range /= lo16(r.w);
       uint32_t code = ((d.code - d.low) / d.range) & 0xFFFF;
-      if (code < r.escapes) {  // end of stream, :674-696
-        d.take(0, r.escapes);
+      if (code < hi16(r.z)) {  // end of stream, :674-696
+        d.take(0, hi16(r.z));
         break;
       }
-      code = (code - r.escapes) & 0xFFFF;
+      code = (code - hi16(r.z)) & 0xFFFF;
       uint32_t under = 0, count = kSymbolMinimum, sym;
-      if (r.symbols == 0) {
+      if (lo16(r.z) == 0) {
         value = (code / kSymbolMinimum) & 0xFF;
         under = (code - code % kSymbolMinimum) & 0xFFFF;
         sym = m.new_symbol(value, kCtxSymbolDelta);
-        m.a[0].symbols = (uint16_t)sym;
+        m.words(0)[2] = pack(sym, hi16(r.z));
       } else {
-        uint32_t i = r.symbols;
+        uint32_t i = lo16(r.z);
         for (;;) {  // :719-796
           const Sym s = m.load(i);
-          const int after = (int)((under + s.under + (s.value + 1u) * kSymbolMinimum) & 0xFFFF);
-          const int before = (int)((s.count + kSymbolMinimum) & 0xFFFF);
+          const uint32_t su = hi16(s.x), sc = sym_count(s), sv = sym_value(s);
+          const int after = (int)((under + su + (sv + 1u) * kSymbolMinimum) & 0xFFFF);
+          const int before = (int)((sc + kSymbolMinimum) & 0xFFFF);
           const int c = (int)code;
           if (c >= after) {
-            under = (under + s.under) & 0xFFFF;
-            if (s.right) {
-              i += s.right;
+            under = (under + su) & 0xFFFF;
+            if (hi16(s.y)) {
+              i += hi16(s.y);
               continue;
             }
-            value = (uint32_t)(s.value + 1 + (c - after) / (int)kSymbolMinimum) & 0xFF;
+            value = (uint32_t)((int)sv + 1 + (c - after) / (int)kSymbolMinimum) & 0xFF;
             under = (uint32_t)(c - (c - after) % (int)kSymbolMinimum) & 0xFFFF;
             sym = m.new_symbol(value, kCtxSymbolDelta);
-            m.a[i].right = (uint16_t)(sym - i);
+            m.words(i)[1] = pack(s.y, sym - i);
             break;
           }
           if (c < after - before) {
-            m.a[i].under = (uint16_t)(s.under + kCtxSymbolDelta);
-            if (s.left) {
-              i += s.left;
+            m.words(i)[0] = pack(s.x, su + kCtxSymbolDelta);
+            if (lo16(s.y)) {
+              i += lo16(s.y);
               continue;
             }
-            value = (uint32_t)(s.value - 1 - (after - before - c - 1) / (int)kSymbolMinimum) & 0xFF;
+            value = (uint32_t)((int)sv - 1 - (after - before - c - 1) / (int)kSymbolMinimum) & 0xFF;
             under = (uint32_t)(c - (after - before - c - 1) % (int)kSymbolMinimum) & 0xFFFF;
             sym = m.new_symbol(value, kCtxSymbolDelta);
-            m.a[i].left = (uint16_t)(sym - i);
+            m.words(i)[1] = pack(sym - i, hi16(s.y));
             break;
           }
-          value = s.value;
-          count = (count + s.count) & 0xFFFF;
+          value = sv;
+          count = (count + sc) & 0xFFFF;
           under = (uint32_t)(after - before) & 0xFFFF;
-          m.a[i].under = (uint16_t)(s.under + kCtxSymbolDelta);
-          m.a[i].count = (uint8_t)(s.count + kCtxSymbolDelta);
+          m.words(i)[0] = sym_x(sv, sc + kCtxSymbolDelta, (su + kCtxSymbolDelta) & 0xFFFF);
           sym = i;
           break;
         }
       }
       bottom = sym;
       const Sym r2 = m.load(0);
-      d.take((uint32_t)r2.escapes + under, count);
-      const uint32_t total = (r2.total + kCtxSymbolDelta) & 0xFFFF;
-      m.a[0].total = (uint16_t)total;
-      if (count > 0xff - 2 * kCtxSymbolDelta + kSymbolMinimum || total > kBottom - 0x100) m.root_rescale();
+      d.take(hi16(r2.z) + under, count);
+      const uint32_t total = (lo16(r2.w) + kCtxSymbolDelta) & 0xFFFF;
+      m.words(0)[3] = pack(total, hi16(r2.w));
+      if (count > 0xff - 2 * kCtxSymbolDelta + kSymbolMinimum || total > kBottom - 0x100)
+        m.ctx_rescale(0, 256 * kSymbolMinimum);
     }
     // patch the higher-order contexts, :841-948
     uint32_t parent = ~0u;
@@ -441,29 +437,17 @@ RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8
       m.set_parent(parent, sym);
       parent = sym;
       const Sym x = m.load(p);
-      uint32_t total = x.total;
+      uint32_t total = lo16(x.w);
       if (count == 0) {
-        m.a[p].escapes = (uint16_t)(x.escapes + kSubEscapeDelta);
+        m.words(p)[2] = pack(x.z, hi16(x.z) + kSubEscapeDelta);
         total = (total + kSubEscapeDelta) & 0xFFFF;
       }
       total = (total + kSubSymbolDelta) & 0xFFFF;
-      m.a[p].total = (uint16_t)total;
-      if (count > 0xff - 2 * kSubSymbolDelta || total > kBottom - 0x100) m.sub_rescale(p);
-      p = x.parent;
+      m.words(p)[3] = pack(total, hi16(x.w));
+      if (count > 0xff - 2 * kSubSymbolDelta || total > kBottom - 0x100) m.ctx_rescale(p, 0);
+      p = hi16(x.w);
     }
     m.set_parent(parent, bottom);
-#ifdef RC_DEBUG_EXITS
-    if (2048 + 16 * (n + 1) <= out_lim) {  // debug trace: per symbol, after the patch loop
-      uint32_t* t = (uint32_t*)(out + 2048 + 16 * n);
-      t[0] = value | (ctx << 8) | (m.predicted << 20);
-      t[1] = d.low;
-      t[2] = d.range;
-      t[3] = d.code;
-    }
-    if (n == 3 && out_lim >= 4096 + 256) {  // debug: arena[0..15] after symbol 3
-      for (int k = 0; k < 16; ++k) *(Sym*)(out + 4096 + 16 * k) = m.a[k];
-    }
-#endif
     if (n >= out_lim) return RC_FAIL(4, n);  // :949-954
     out[n++] = (uint8_t)value;
     m.advance();
