@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident CRC-32 throughput over ENet packet batches (BASELINE.json).
 
-    python bench.py [--gpus N --steps K --warmup W --config uniform|ragged|large]
+    python bench.py [--gpus N --steps K --warmup W --config uniform|ragged|large|range]
 
 One step = one launch of the batch kernel over this rank's whole shard, inputs
 already resident in HBM.  Default workload: 1M x 1200-byte packets on 1 GPU
@@ -11,6 +11,11 @@ configs[3] (16M x 1200 B sharded 8 ways).  One process per GPU
 work is fixed as N grows: weak scaling.  Rank 0 prints one JSON line, which at
 N = 1 also carries the CPU baseline (oracle on the host cores) and the
 end-to-end host->device->host rate of the host-memory entry point.
+
+--config range measures the batched ENet range coder instead:
+one step = one compress launch over 1M ragged U{64..1392} compressible packets
+(the configs[2] shape); the line also carries the decompress rate and the oracle
+(src/c/compress.rs restated in C) timed on one host core.
 """
 from __future__ import annotations
 
@@ -29,7 +34,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 import rusty_enet_amd as rea  # noqa: E402
 from rusty_enet_amd.shards import max_over_ranks  # noqa: E402
-from _data import ENET_SEED, packed_offsets, ragged_lengths  # noqa: E402
+from _data import ENET_SEED, enet_like_bytes, packed_offsets, ragged_lengths  # noqa: E402
 
 METRIC = "device-resident GiB/s, batched CRC-32 over ENet packets; % HBM3E peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -41,7 +46,11 @@ CONFIGS = {
     "ragged": ("ragged packets, lengths U{64..1392}, packed at byte offsets; BASELINE configs[2]",
                1 << 20, 1 << 20),
     "large": ("64 KiB buffers, one CRC each (large-buffer path); BASELINE configs[4]", 32768, 32768),
+    "range": ("ragged compressible packets, lengths U{64..1392}, range-coder compress (SURVEY.md 8(f)4)",
+              1 << 20, 1 << 20),
 }
+RANGE_METRIC = "device-resident GiB/s, batched ENet range-coder compress (uncompressed input bytes)"
+RANGE_WORKERS = 1 << 19  # concurrent coders: 8 waves/SIMD x 4 SIMDs x 64 lanes x 256 CUs (32 GiB arenas)
 
 
 def packets_per_gpu(name: str, world: int) -> int:
@@ -68,6 +77,17 @@ def make_workload(name: str, rank: int, world: int, dev):
     lengths = ragged_lengths(ENET_SEED + rank, n)
     offsets = packed_offsets(lengths)
     total = int(lengths.sum())
+    if name == "range":
+        host = enet_like_bytes(ENET_SEED + rank, total)
+        data = torch.from_numpy(host).to(dev)
+        off = torch.from_numpy(offsets.astype(np.int64)).to(dev)
+        ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
+        res = {}
+
+        def step():
+            res["out"] = rea.compress_batch(data, off, ln, workers=RANGE_WORKERS)
+
+        return step, total, n, res, ("range", host, offsets, lengths, data, off, ln)
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
     off = torch.from_numpy(offsets.astype(np.int64)).to(dev)
     ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
@@ -80,6 +100,22 @@ def verify_sample(out, spec, limit=20000) -> None:
     """Bit-exact check of a sample of this rank's outputs against the oracle (not timed)."""
     import _oracle
 
+    if spec[0] == "range":
+        import _range_oracle as ro
+
+        _, host, offsets, lengths = spec[:4]
+        c_out, c_off, c_sizes = out["out"]
+        m = min(len(lengths), 4000)
+        o_out, o_sizes = ro.compress_ragged(host, offsets[:m], lengths[:m], packed_offsets(lengths[:m]), lengths[:m])
+        g_sizes = c_sizes[:m].cpu().numpy().astype(np.uint32)
+        g_out, g_off = c_out.cpu().numpy(), c_off[:m].cpu().numpy()
+        o_off = packed_offsets(lengths[:m])
+        bad = int(np.count_nonzero(g_sizes != o_sizes))
+        bad += sum(g_out[int(g_off[p]):int(g_off[p]) + int(g_sizes[p])].tobytes() !=
+                   o_out[int(o_off[p]):int(o_off[p]) + int(o_sizes[p])].tobytes() for p in range(m))
+        if bad:
+            raise SystemExit(f"bench: {bad} of {m} range-coded packets differ from the oracle")
+        return
     got = out.cpu().numpy().view(np.uint32)
     if spec[0] == "uniform":
         _, data, stride, length, n = spec
@@ -123,6 +159,51 @@ def cpu_baseline(seconds: float = 10.0) -> dict:
             "sample": f"4096 x 1200 B (BASELINE configs[0]), one crc32 call per packet, median of "
                       f"{len(times)} passes over ~{seconds:.0f} s; C restatement of src/crc32.rs (no rustc here)",
             "all_cores": {"value": round(multi, 4), "cores": threads}}
+
+
+def range_cpu_baseline(spec, seconds: float = 5.0) -> dict:
+    """src/c/compress.rs restated in C (oracle/range_coder_oracle.c) on one host core."""
+    import _range_oracle as ro
+
+    _, host, offsets, lengths = spec[:4]
+    k = 4096
+    nb = int(lengths[:k].sum())
+    end = int(offsets[k - 1]) + int(lengths[k - 1])
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        ro.compress_ragged(host[:end], offsets[:k], lengths[:k], packed_offsets(lengths[:k]), lengths[:k])
+        times.append(time.perf_counter() - t0)
+    return {"value": round(nb / float(np.median(times)) / 2**30, 5), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"first 4096 packets of the workload ({nb} B), one compress call per packet, median of "
+                      f"{len(times)} passes; C restatement of src/c/compress.rs (no rustc here)"}
+
+
+def range_decompress_rate(spec, res, steps: int = 3) -> dict:
+    """Decompress the step's coded packets back (device-resident), timed on the current stream."""
+    _, host, offsets, lengths, data, off, ln = spec
+    c_out, c_off, c_sizes = res["out"]
+    dev = c_out.device
+    coded = c_sizes > 0
+    idx = torch.nonzero(coded).flatten()
+    d_len = c_sizes[idx]
+    d_off = c_off[idx]
+    lim = ln[idx]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = rea.decompress_batch(c_out, d_off, d_len, lim, workers=RANGE_WORKERS)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(out[2][:1000].to(torch.int64), lim[:1000].to(torch.int64)))
+    ev0.record()
+    for _ in range(steps):
+        rea.decompress_batch(c_out, d_off, d_len, lim, workers=RANGE_WORKERS)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / steps
+    nb = int(lim.to(torch.int64).sum().item())
+    return {"value": round(nb / (ms / 1e3) / 2**30, 4), "unit": "GiB/s", "ms": round(ms, 3),
+            "packets": int(idx.numel()), "sizes_match_inputs": ok,
+            "compressed_fraction": round(float(c_sizes.to(torch.int64).sum().item()) / float(ln.to(torch.int64).sum().item()), 4)}
 
 
 def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
@@ -207,13 +288,18 @@ def load_pmc_traffic(config: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 200; 5 for --config range)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 10; 1 for --config range)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="uniform")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host-memory measurement")
     args = ap.parse_args()
+    is_range = args.config == "range"
+    if args.steps is None:
+        args.steps = 5 if is_range else 200
+    if args.warmup is None:
+        args.warmup = 1 if is_range else 10
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -260,7 +346,7 @@ def main() -> None:
         achieved = nbytes / (kernel_ms / 1000.0) / 1e9  # per-GPU algorithmic GB/s (rank 0)
         traffic = load_pmc_traffic(args.config)
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "metric": RANGE_METRIC if is_range else METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (torch.randint bytes on device, seeded)",
@@ -272,9 +358,16 @@ def main() -> None:
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel_ms": round(kernel_ms, 5), "kernel_ms_max_rank": round(kernel_ms_max, 5)},
         }
+        if is_range:
+            line["config"]["workers"] = RANGE_WORKERS
+            line["data"] = "synthetic compressible ENet-like bytes (tests/_data.enet_like_bytes, seeded)"
+            line["roofline"]["note"] = ("latency-bound (dependent arena loads per byte); achieved = "
+                                        "uncompressed input bytes per launch / launch time")
+            if world == 1:
+                line["decompress"] = range_decompress_rate(spec, out)
         if world == 1 and args.cpu_seconds > 0:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        if world == 1 and not args.no_e2e:
+            line["cpu_baseline"] = range_cpu_baseline(spec) if is_range else cpu_baseline(args.cpu_seconds)
+        if world == 1 and not args.no_e2e and not is_range:
             line["end_to_end"] = end_to_end(dev)
         print(json.dumps(line), flush=True)
     if world > 1:
