@@ -6,11 +6,17 @@
 One step = one launch of the batch kernel over this rank's whole shard, inputs
 already resident in HBM.  Default workload: 1M x 1200-byte packets on 1 GPU
 (BASELINE configs[1]); with N > 1 GPUs each rank takes 2M packets, so N = 8 is
-configs[3] (16M x 1200 B sharded 8 ways).  One process per GPU
-(torch.distributed.run); shards are independent (no data-path collective), per-GPU
-work is fixed as N grows: weak scaling.  Rank 0 prints one JSON line, which at
-N = 1 also carries the CPU baseline (oracle on the host cores) and the
-end-to-end host->device->host rate of the host-memory entry point.
+configs[3] (16M x 1200 B sharded 8 ways).  At N = 1 the line also times the same
+2M-packet shard (``shard_2m``), so the per-GPU work behind the N = 1 and N > 1
+numbers can be compared like for like.
+
+Multi-GPU: one process per GPU.  ``--gpus N`` without an enclosing torchrun
+starts ``torch.distributed.run`` with N ranks as a child process (before anything
+touches the GPU) and exits with its status; under torchrun, ``--gpus`` must equal
+WORLD_SIZE.  Shards are independent (no data-path collective); the max-over-ranks
+timing uses a gloo process group on the CPU.  Per-GPU work is fixed as N grows:
+weak scaling.  Rank 0 prints one JSON line, which at N = 1 also carries the CPU
+baseline (oracle on the host cores) and the end-to-end host->device->host rates.
 
 --config range measures the batched ENet range coder instead:
 one step = one compress launch over 1M ragged U{64..1392} compressible packets
@@ -20,24 +26,25 @@ one step = one compress launch over 1M ragged U{64..1392} compressible packets
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
-import rusty_enet_amd as rea  # noqa: E402
-from rusty_enet_amd.shards import max_over_ranks  # noqa: E402
-from _data import ENET_SEED, enet_like_bytes, packed_offsets, ragged_lengths  # noqa: E402
-
 METRIC = "device-resident GiB/s, batched CRC-32 over ENet packets; % HBM3E peak"
+RANGE_METRIC = "device-resident GiB/s, batched ENet range-coder compress (uncompressed input bytes)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+RANGE_WORKERS = 1 << 19  # concurrent range coders: 8 waves/SIMD x 4 SIMDs x 64 lanes x 256 CUs
 
 CONFIGS = {
     # name: (description, packets per GPU at N = 1, packets per GPU at N > 1)
@@ -49,27 +56,65 @@ CONFIGS = {
     "range": ("ragged compressible packets, lengths U{64..1392}, range-coder compress (SURVEY.md 8(f)4)",
               1 << 20, 1 << 20),
 }
-RANGE_METRIC = "device-resident GiB/s, batched ENet range-coder compress (uncompressed input bytes)"
-RANGE_WORKERS = 1 << 19  # concurrent coders: 8 waves/SIMD x 4 SIMDs x 64 lanes x 256 CUs (32 GiB arenas)
+# Source files whose change invalidates a committed traffic measurement.
+KERNEL_SOURCES = ("crc32_kernels.hip", "crc32_geometry.hpp", "crc32_layout.hpp", "crc32_ops.hpp",
+                  "crc32_kernels.hpp", "range_coder.hip", "range_coder.hpp")
 
 
-def packets_per_gpu(name: str, world: int) -> int:
+def packets_per_gpu(name: str, world: int, override: int | None = None) -> int:
+    if override:
+        return override
     _, n1, nn = CONFIGS[name]
     return n1 if world == 1 else nn
 
 
-def make_workload(name: str, rank: int, world: int, dev):
+# --------------------------------------------------------------------------------------
+# multi-process launch
+# --------------------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_command(gpus: int, argv: list[str], port: int) -> list[str]:
+    """torch.distributed.run command that re-runs this script with `gpus` ranks."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def visible_gpus() -> int:
+    import torch
+
+    return torch.cuda.device_count()  # does not initialise the GPU on this image
+
+
+def spawn(args, argv: list[str]) -> int:
+    """Start N ranks as a child process group (nothing here has touched the GPU)."""
+    have = visible_gpus()
+    if have < args.gpus:
+        print(f"bench: --gpus {args.gpus} requested but only {have} HIP device(s) are visible",
+              file=sys.stderr, flush=True)
+        return 2
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(spawn_command(args.gpus, argv, _free_port()), env=env)
+
+
+# --------------------------------------------------------------------------------------
+# workloads
+# --------------------------------------------------------------------------------------
+
+def make_workload(name: str, rank: int, n: int, dev):
+    import torch
+
+    import rusty_enet_amd as rea
+    from _data import ENET_SEED, enet_like_bytes, packed_offsets, ragged_lengths
+
     g = torch.Generator(device=dev)
     g.manual_seed(ENET_SEED + 7919 * rank)
-    n = packets_per_gpu(name, world)
-    if name == "uniform":
-        L = 1200
-        data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
-        out = torch.empty(n, dtype=torch.int32, device=dev)
-        step = lambda: rea.crc32_batch(data, stride=L, length=L, count=n, out=out)  # noqa: E731
-        return step, n * L, n, out, ("uniform", data, L, L, n)
-    if name == "large":
-        L = 65536
+    if name in ("uniform", "large"):
+        L = 1200 if name == "uniform" else 65536
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         step = lambda: rea.crc32_batch(data, stride=L, length=L, count=n, out=out)  # noqa: E731
@@ -99,6 +144,7 @@ def make_workload(name: str, rank: int, world: int, dev):
 def verify_sample(out, spec, limit=20000) -> None:
     """Bit-exact check of a sample of this rank's outputs against the oracle (not timed)."""
     import _oracle
+    from _data import packed_offsets
 
     if spec[0] == "range":
         import _range_oracle as ro
@@ -131,10 +177,44 @@ def verify_sample(out, spec, limit=20000) -> None:
         raise SystemExit(f"bench: {int(np.count_nonzero(got[:m] != want))} of {m} checksums differ from the oracle")
 
 
+# --------------------------------------------------------------------------------------
+# CPU baseline
+# --------------------------------------------------------------------------------------
+
+def host_cpus() -> dict:
+    """What this process may run on: `nproc` (the affinity mask), the cgroup CPU quota,
+    the machine's CPU count and the CPU model."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        nproc = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    threads = nproc if quota is None else max(1, min(nproc, int(math.ceil(quota))))
+    threads = min(threads, 256)  # the oracle's thread limit (oracle/crc32_oracle.c)
+    return {"model": model, "nproc": nproc, "cgroup_cpus": quota, "machine_cpus": os.cpu_count(),
+            "threads": threads}
+
+
 def cpu_baseline(seconds: float = 10.0) -> dict:
     """src/crc32.rs restated in C (oracle/), timed on this host: BASELINE configs[0]."""
     import _oracle
-    from _data import splitmix64_bytes
+    from _data import ENET_SEED, splitmix64_bytes
 
     n, L = 4096, 1200
     data = splitmix64_bytes(ENET_SEED, n * L)
@@ -146,24 +226,31 @@ def cpu_baseline(seconds: float = 10.0) -> dict:
         _oracle.crc32_uniform(data, L, L, n)
         times.append(time.perf_counter() - t0)
     single = n * L / float(np.median(times)) / 2**30
-    threads = max(1, min(os.cpu_count() or 1, 16))
+    cpus = host_cpus()
+    threads = cpus["threads"]
+    reps = max(8, 2 * threads)  # every thread gets >= 2 x 4096 packets
+    big = np.tile(data, reps)
     mt_times = []
-    big = np.tile(data, 8)  # 32768 packets so every thread has work
-    t_end = time.perf_counter() + seconds / 4
+    t_end = time.perf_counter() + seconds / 2
     while time.perf_counter() < t_end or len(mt_times) < 10:
         t0 = time.perf_counter()
-        _oracle.crc32_uniform(big, L, L, 8 * n, threads=threads)
+        _oracle.crc32_uniform(big, L, L, reps * n, threads=threads)
         mt_times.append(time.perf_counter() - t0)
-    multi = 8 * n * L / float(np.median(mt_times)) / 2**30
+    multi = reps * n * L / float(np.median(mt_times)) / 2**30
     return {"value": round(single, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"4096 x 1200 B (BASELINE configs[0]), one crc32 call per packet, median of "
                       f"{len(times)} passes over ~{seconds:.0f} s; C restatement of src/crc32.rs (no rustc here)",
-            "all_cores": {"value": round(multi, 4), "cores": threads}}
+            "cpu_model": cpus["model"],
+            "all_cores": {"value": round(multi, 4), "unit": "GiB/s", "cores": threads,
+                          "sample": f"{reps} x 4096 x 1200 B split over {threads} threads "
+                                    f"(nproc {cpus['nproc']}, cgroup quota {cpus['cgroup_cpus']}, "
+                                    f"machine CPUs {cpus['machine_cpus']}), median of {len(mt_times)} passes"}}
 
 
 def range_cpu_baseline(spec, seconds: float = 5.0) -> dict:
     """src/c/compress.rs restated in C (oracle/range_coder_oracle.c) on one host core."""
     import _range_oracle as ro
+    from _data import packed_offsets
 
     _, host, offsets, lengths = spec[:4]
     k = 4096
@@ -176,15 +263,23 @@ def range_cpu_baseline(spec, seconds: float = 5.0) -> dict:
         ro.compress_ragged(host[:end], offsets[:k], lengths[:k], packed_offsets(lengths[:k]), lengths[:k])
         times.append(time.perf_counter() - t0)
     return {"value": round(nb / float(np.median(times)) / 2**30, 5), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "cpu_model": host_cpus()["model"],
             "sample": f"first 4096 packets of the workload ({nb} B), one compress call per packet, median of "
                       f"{len(times)} passes; C restatement of src/c/compress.rs (no rustc here)"}
 
 
+# --------------------------------------------------------------------------------------
+# secondary measurements (N = 1 only)
+# --------------------------------------------------------------------------------------
+
 def range_decompress_rate(spec, res, steps: int = 3) -> dict:
     """Decompress the step's coded packets back (device-resident), timed on the current stream."""
+    import torch
+
+    import rusty_enet_amd as rea
+
     _, host, offsets, lengths, data, off, ln = spec
     c_out, c_off, c_sizes = res["out"]
-    dev = c_out.device
     coded = c_sizes > 0
     idx = torch.nonzero(coded).flatten()
     d_len = c_sizes[idx]
@@ -203,14 +298,17 @@ def range_decompress_rate(spec, res, steps: int = 3) -> dict:
     nb = int(lim.to(torch.int64).sum().item())
     return {"value": round(nb / (ms / 1e3) / 2**30, 4), "unit": "GiB/s", "ms": round(ms, 3),
             "packets": int(idx.numel()), "sizes_match_inputs": ok,
-            "compressed_fraction": round(float(c_sizes.to(torch.int64).sum().item()) / float(ln.to(torch.int64).sum().item()), 4)}
+            "compressed_fraction": round(float(c_sizes.to(torch.int64).sum().item()) /
+                                         float(ln.to(torch.int64).sum().item()), 4)}
 
 
 def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
     """Host buffers -> pinned staging -> H2D -> kernel -> D2H (enet_crc32_ragged_host),
     plus the per-call latency of the drop-in hook (enet_crc32_iov, one datagram)."""
     import _oracle
-    from _data import splitmix64_bytes
+    from _data import ENET_SEED, splitmix64_bytes
+
+    import rusty_enet_amd as rea
 
     data = splitmix64_bytes(ENET_SEED + 99, n * L)
     off = np.arange(n, dtype=np.uint64) * np.uint64(L)
@@ -228,6 +326,8 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
         times.append(time.perf_counter() - t0)
     rate = n * L / float(np.median(times)) / 2**30
     pkt = [data[:1392]]
+    if ctx.crc32(pkt) != _oracle.crc32(pkt):
+        raise SystemExit("bench: per-call checksum differs from the oracle")
     for _ in range(50):
         ctx.crc32(pkt)
     t0 = time.perf_counter()
@@ -247,7 +347,8 @@ def ring_rate(dev, L: int = 1200, nslots: int = 4, per_slot: int = 40000, rounds
     """Pinned receive ring (enet_crc_ring_*): packets already in pinned slot memory,
     H2D + kernel + D2H of each slot on its own stream, slots overlapped."""
     import _oracle
-    from _data import splitmix64_bytes
+    from _data import ENET_SEED, splitmix64_bytes
+
     from rusty_enet_amd.ring import ReceiveRing
 
     with ReceiveRing(dev.index or 0, nslots=nslots, slot_bytes=per_slot * L, slot_packets=per_slot) as ring:
@@ -275,55 +376,37 @@ def ring_rate(dev, L: int = 1200, nslots: int = 4, per_slot: int = 40000, rounds
             "sample": f"{nslots} pinned slots x {per_slot} x {L} B, {rounds} rounds of submit-all/wait-all"}
 
 
+# --------------------------------------------------------------------------------------
+# roofline evidence
+# --------------------------------------------------------------------------------------
+
+def kernel_source_hash() -> str:
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        path = os.path.join(REPO, "rusty_enet_amd", "csrc", name)
+        if os.path.exists(path):
+            with open(path, "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def load_pmc_traffic(config: str):
+    """HBM bytes per launch of the dominant kernel from profiles/pmc_traffic.json, but only
+    when it was measured on the kernel sources as they are now (else None)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             v = json.load(f).get(config)
-        return None if v is None else v.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        return None
+        return None, None
+    if not v or v.get("source_hash") != kernel_source_hash():
+        return None, None
+    return v.get("hbm_bytes_per_launch"), v.get("source")
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 200; 5 for --config range)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 10; 1 for --config range)")
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="uniform")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host-memory measurement")
-    args = ap.parse_args()
-    is_range = args.config == "range"
-    if args.steps is None:
-        args.steps = 5 if is_range else 200
-    if args.warmup is None:
-        args.warmup = 1 if is_range else 10
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    step, nbytes, npk, out, spec = make_workload(args.config, rank, world, dev)
-    step()
-    torch.cuda.synchronize()
-    if not args.no_verify:
-        verify_sample(out, spec)
-    for _ in range(args.warmup):
-        step()
-
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
+def time_steps(step, steps: int, barrier, dev) -> tuple[float, float]:
+    """(wall seconds, mean ms per launch on the launch stream) over exactly `steps` steps."""
+    import torch
 
     stream = torch.cuda.current_stream(dev)  # the stream crc32_batch launches on
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -331,35 +414,124 @@ def main() -> None:
     barrier()
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     ev1.record(stream)
     barrier()
     wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # average launch duration on that stream
-    wall_max, kernel_ms_max = max_over_ranks([wall, kernel_ms], device=dev)
+    return wall, ev0.elapsed_time(ev1) / steps
+
+
+def shard_2m(dev, rank: int, steps: int, warmup: int, barrier) -> dict:
+    """The N > 1 per-GPU shard (2M x 1200 B) timed on this GPU, at N = 1."""
+    import torch
+
+    n = CONFIGS["uniform"][2]
+    step, nbytes, _, out, spec = make_workload("uniform", rank, n, dev)
+    step()
+    torch.cuda.synchronize()
+    verify_sample(out, spec)
+    for _ in range(warmup):
+        step()
+    wall, kms = time_steps(step, steps, barrier, dev)
+    ms = wall * 1000.0 / steps
+    res = {"packets": n, "bytes": nbytes, "ms_per_step": round(ms, 5),
+           "value": round(nbytes / (ms / 1000.0) / 2**30, 2), "unit": "GiB/s",
+           "kernel_ms": round(kms, 5), "frac": round(nbytes / (kms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
+    del spec, out
+    torch.cuda.empty_cache()
+    return res
+
+
+# --------------------------------------------------------------------------------------
+
+def parse_args(argv):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default WORLD_SIZE or 1")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 200; 5 for --config range)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 10; 1 for --config range)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="uniform")
+    ap.add_argument("--packets-per-gpu", type=int, default=None,
+                    help="override the per-GPU packet count (default: 1M at N = 1, 2M at N > 1 for uniform)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host-memory measurement")
+    ap.add_argument("--no-shard", action="store_true", help="skip the 2M-packet shard measurement at N = 1")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        return spawn(args, argv)
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        return 2
+    is_range = args.config == "range"
+    if args.steps is None:
+        args.steps = 5 if is_range else 200
+    if args.warmup is None:
+        args.warmup = 1 if is_range else 10
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")  # timing reduction only; no data-path collective
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+
+    npk = packets_per_gpu(args.config, world, args.packets_per_gpu)
+    step, nbytes, npk, out, spec = make_workload(args.config, rank, npk, dev)
+    step()
+    torch.cuda.synchronize()
+    if not args.no_verify:
+        verify_sample(out, spec)
+    for _ in range(args.warmup):
+        step()
+    wall, kernel_ms = time_steps(step, args.steps, barrier, dev)
+
+    from rusty_enet_amd.shards import max_over_ranks
+
+    wall_max, kernel_ms_max = max_over_ranks([wall, kernel_ms])
     ms_per_step = wall_max * 1000.0 / args.steps
+    extra = {}
+    if world == 1 and args.config == "uniform" and not args.no_shard and not args.packets_per_gpu:
+        del step, out, spec
+        torch.cuda.empty_cache()
+        extra["shard_2m"] = shard_2m(dev, rank, min(args.steps, 100), args.warmup, barrier)
 
     if rank == 0:
         total_bytes = nbytes * world
         value = total_bytes / (ms_per_step / 1000.0) / 2**30
         achieved = nbytes / (kernel_ms / 1000.0) / 1e9  # per-GPU algorithmic GB/s (rank 0)
-        traffic = load_pmc_traffic(args.config)
+        traffic, traffic_src = load_pmc_traffic(args.config)
         line = {
-            "metric": RANGE_METRIC if is_range else METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "metric": RANGE_METRIC if is_range else METRIC, "value": round(value, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (torch.randint bytes on device, seeded)",
             "config": {"workload": f"{npk} x " + CONFIGS[args.config][0] + " per GPU", "packets_per_gpu": npk,
-                       "bytes_per_gpu": nbytes,
-                       "parallelism": f"{world} independent shards, no collective"},
+                       "bytes_per_gpu": nbytes, "parallelism": f"{world} independent shards, no collective"},
             "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "kernel_source_hash": kernel_source_hash(),
                          "kernel_ms": round(kernel_ms, 5), "kernel_ms_max_rank": round(kernel_ms_max, 5)},
         }
+        line.update(extra)
         if is_range:
-            line["config"]["workers"] = RANGE_WORKERS
             line["data"] = "synthetic compressible ENet-like bytes (tests/_data.enet_like_bytes, seeded)"
             line["roofline"]["note"] = ("latency-bound (dependent arena loads per byte); achieved = "
                                         "uncompressed input bytes per launch / launch time")
@@ -371,8 +543,10 @@ def main() -> None:
             line["end_to_end"] = end_to_end(dev)
         print(json.dumps(line), flush=True)
     if world > 1:
+        torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

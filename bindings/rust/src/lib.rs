@@ -29,6 +29,23 @@ pub struct enet_crc_ctx {
 }
 
 pub const ENET_CRC_OK: c_int = 0;
+pub const ENET_CRC_PERCALL_COPY: c_int = 0;
+pub const ENET_CRC_PERCALL_ZEROCOPY: c_int = 1;
+
+/// `enet_crc_shard` (include/enet_crc_amd.h): one device-resident batch of a
+/// multi-device launch.  `d_offsets == null` means a uniform shard.
+#[repr(C)]
+pub struct enet_crc_shard {
+    pub device: c_int,
+    pub d_base: *const c_void,
+    pub d_offsets: *const u64,
+    pub d_lengths: *const u32,
+    pub stride: u64,
+    pub length: u32,
+    pub count: u64,
+    pub d_out: *mut u32,
+    pub hip_stream: *mut c_void,
+}
 
 extern "C" {
     pub fn enet_crc_abi_version() -> c_int;
@@ -36,7 +53,12 @@ extern "C" {
     pub fn enet_crc_last_hip_error() -> c_int;
     pub fn enet_crc_device_count() -> c_int;
     pub fn enet_crc_ctx_create(device: c_int, out_ctx: *mut *mut enet_crc_ctx) -> c_int;
+    pub fn enet_crc_ctx_create_multi(devices: *const c_int, ndevices: u32, out_ctx: *mut *mut enet_crc_ctx) -> c_int;
     pub fn enet_crc_ctx_destroy(ctx: *mut enet_crc_ctx);
+    pub fn enet_crc_ctx_lanes(ctx: *const enet_crc_ctx) -> c_int;
+    pub fn enet_crc_ctx_set_percall_mode(ctx: *mut enet_crc_ctx, mode: c_int) -> c_int;
+    pub fn enet_crc_shard_bounds(lengths: *const u32, count: u64, nshards: u32, bounds: *mut u64) -> c_int;
+    pub fn enet_crc32_shards_device(shards: *const enet_crc_shard, nshards: usize) -> c_int;
     pub fn enet_crc32_iov(ctx: *mut enet_crc_ctx, bufs: *const enet_crc_iov, nbufs: usize, out_crc: *mut u32) -> c_int;
     pub fn enet_crc32_uniform_device(d_base: *const c_void, stride: u64, length: u32, count: u64,
                                      d_out: *mut u32, hip_stream: *mut c_void) -> c_int;
@@ -51,6 +73,35 @@ extern "C" {
                                            d_slot_offsets: *const u32, d_slot_values: *const u32, count: u64,
                                            d_crc: *mut u32, hip_stream: *mut c_void) -> c_int;
     pub fn enet_crc32_slot_adjust(crc: u32, old_slot: u32, new_slot: u32, bytes_after_slot: u32) -> u32;
+
+    // include/enet_range_amd.h
+    pub fn enet_range_scratch_bytes(workers: u64) -> u64;
+    pub fn enet_range_compress_iov(ctx: *mut enet_crc_ctx, bufs: *const enet_crc_iov, nbufs: usize, in_limit: usize,
+                                   out: *mut u8, out_limit: usize, out_size: *mut usize) -> c_int;
+    pub fn enet_range_decompress(ctx: *mut enet_crc_ctx, input: *const u8, in_len: usize, out: *mut u8,
+                                 out_limit: usize, out_size: *mut usize) -> c_int;
+    pub fn enet_range_compress_ragged_host(ctx: *mut enet_crc_ctx, h_in: *const c_void, h_in_offsets: *const u64,
+                                           h_in_lengths: *const u32, count: u64, h_out: *mut c_void,
+                                           h_out_offsets: *const u64, h_out_limits: *const u32,
+                                           h_sizes: *mut u32) -> c_int;
+    pub fn enet_range_decompress_ragged_host(ctx: *mut enet_crc_ctx, h_in: *const c_void, h_in_offsets: *const u64,
+                                             h_in_lengths: *const u32, count: u64, h_out: *mut c_void,
+                                             h_out_offsets: *const u64, h_out_limits: *const u32,
+                                             h_sizes: *mut u32) -> c_int;
+    pub fn enet_range_compress_ragged_device(d_in: *const c_void, d_in_offsets: *const u64,
+                                             d_in_lengths: *const u32, count: u64, d_out: *mut c_void,
+                                             d_out_offsets: *const u64, d_out_limits: *const u32, d_sizes: *mut u32,
+                                             d_scratch: *mut c_void, scratch_bytes: u64,
+                                             hip_stream: *mut c_void) -> c_int;
+    pub fn enet_range_decompress_ragged_device(d_in: *const c_void, d_in_offsets: *const u64,
+                                               d_in_lengths: *const u32, count: u64, d_out: *mut c_void,
+                                               d_out_offsets: *const u64, d_out_limits: *const u32,
+                                               d_sizes: *mut u32, d_scratch: *mut c_void, scratch_bytes: u64,
+                                               hip_stream: *mut c_void) -> c_int;
+}
+
+fn last_error(status: c_int) -> CrcError {
+    CrcError { status, hip_error: unsafe { enet_crc_last_hip_error() } }
 }
 
 /// Checksum of a datagram after its 4-byte checksum slot changes from `old_slot` to
@@ -85,12 +136,29 @@ pub struct GpuCrc32 {
 
 impl GpuCrc32 {
     pub fn new(device: i32) -> Result<Self, CrcError> {
+        Self::with_devices(&[device])
+    }
+
+    /// A context over several GPUs (or lanes on one GPU: a device may repeat).  Host
+    /// batches (`crc32_ragged_host`) are split into one byte-balanced shard per entry
+    /// and checksummed on all of them at once.
+    pub fn with_devices(devices: &[i32]) -> Result<Self, CrcError> {
         let mut p = core::ptr::null_mut();
-        let st = unsafe { enet_crc_ctx_create(device, &mut p) };
+        let st = unsafe { enet_crc_ctx_create_multi(devices.as_ptr(), devices.len() as u32, &mut p) };
         if st != ENET_CRC_OK {
-            return Err(CrcError { status: st, hip_error: unsafe { enet_crc_last_hip_error() } });
+            return Err(last_error(st));
         }
         Ok(Self { ctx: Arc::new(Ctx(p)) })
+    }
+
+    /// Every visible GPU of the node, one lane each.
+    pub fn all_devices() -> Result<Self, CrcError> {
+        let n = unsafe { enet_crc_device_count() };
+        if n <= 0 {
+            return Err(last_error(if n == 0 { -2 } else { n }));
+        }
+        let devs: Vec<i32> = (0..n).collect();
+        Self::with_devices(&devs)
     }
 
     /// Same contract as `rusty_enet::crc32` (src/crc32.rs:39), but fallible.
@@ -130,6 +198,61 @@ impl GpuCrc32 {
     }
 }
 
+/// The `Compressor` of rusty_enet (src/compressor.rs:9-14) on the GPU: the range coder
+/// of src/c/compress.rs, run by the `enet_range_*` entry points on a context that owns
+/// the arenas.  Install with `HostSettings { compressor: Some(Box::new(gpu_rc)), .. }`.
+pub struct GpuRangeCoder {
+    ctx: Arc<Ctx>,
+}
+
+impl GpuRangeCoder {
+    pub fn new(device: i32) -> Result<Self, CrcError> {
+        Ok(Self { ctx: GpuCrc32::new(device)?.ctx })
+    }
+
+    /// Shares a checksum context (and so its device, lock and staging).
+    pub fn from_crc(gpu: &GpuCrc32) -> Self {
+        Self { ctx: gpu.ctx.clone() }
+    }
+
+    pub fn try_compress(&self, in_buffers: &[&[u8]], in_limit: usize, out: &mut [u8]) -> Result<usize, CrcError> {
+        let iov: Vec<enet_crc_iov> =
+            in_buffers.iter().map(|b| enet_crc_iov { data: b.as_ptr(), len: b.len() }).collect();
+        let mut n = 0usize;
+        let st = unsafe {
+            enet_range_compress_iov(self.ctx.0, iov.as_ptr(), iov.len(), in_limit, out.as_mut_ptr(), out.len(), &mut n)
+        };
+        if st != ENET_CRC_OK {
+            return Err(last_error(st));
+        }
+        Ok(n)
+    }
+
+    pub fn try_decompress(&self, in_data: &[u8], out: &mut [u8]) -> Result<usize, CrcError> {
+        let mut n = 0usize;
+        let st = unsafe {
+            enet_range_decompress(self.ctx.0, in_data.as_ptr(), in_data.len(), out.as_mut_ptr(), out.len(), &mut n)
+        };
+        if st != ENET_CRC_OK {
+            return Err(last_error(st));
+        }
+        Ok(n)
+    }
+}
+
+/// `impl rusty_enet::Compressor for GpuRangeCoder` (enable the `rusty_enet` feature).
+/// The trait has no error channel; a device failure panics (no CPU fallback).
+#[cfg(feature = "rusty_enet")]
+impl rusty_enet::Compressor for GpuRangeCoder {
+    fn compress(&mut self, in_buffers: &[&[u8]], in_limit: usize, out: &mut [u8]) -> usize {
+        self.try_compress(in_buffers, in_limit, out).expect("enet_crc_amd: GPU range coder failed")
+    }
+
+    fn decompress(&mut self, in_data: &[u8], out: &mut [u8]) -> usize {
+        self.try_decompress(in_data, out).expect("enet_crc_amd: GPU range coder failed")
+    }
+}
+
 #[cfg(test)]
 mod test {
     // The reference's own known answers, src/crc32.rs:49-57.
@@ -138,5 +261,17 @@ mod test {
         let gpu = super::GpuCrc32::new(0).unwrap();
         assert_eq!(gpu.crc32(&[&[1, 2, 3, 4, 5, 6, 7, 8]]).unwrap(), 3314076223);
         assert_eq!(gpu.crc32(&[&[1, 2, 3, 4, 5, 6, 7, 8], &[8, 7, 6, 5, 4, 3, 2, 1]]).unwrap(), 1712484799);
+    }
+
+    #[test]
+    fn range_round_trip() {
+        let rc = super::GpuRangeCoder::new(0).unwrap();
+        let data: Vec<u8> = (0..1000u32).map(|i| (i % 7) as u8).collect();
+        let mut out = vec![0u8; 1000];
+        let n = rc.try_compress(&[&data], data.len(), &mut out).unwrap();
+        assert!(n > 0 && n < data.len());
+        let mut back = vec![0u8; 4096];
+        let m = rc.try_decompress(&out[..n], &mut back).unwrap();
+        assert_eq!(&back[..m], &data[..]);
     }
 }

@@ -19,10 +19,12 @@
  *   - "*_device" functions take device pointers and a hipStream_t passed as
  *     void* (NULL = the legacy default stream); they are asynchronous and
  *     run on the calling thread's current HIP device.
- *   - A context (enet_crc_ctx) owns a stream plus pinned/device staging for
- *     the host-memory entry points.  Calls on one context are serialised by
- *     an internal lock, which is what lets the Rust adapter present it as the
- *     `Fn` (not `FnMut`) closure HostSettings::checksum requires.
+ *     (An explicit stream's own device is used, whatever device is current.)
+ *   - A context (enet_crc_ctx) owns, per entry of its device list, a stream pair
+ *     plus pinned/device staging for the host-memory entry points.  Calls on
+ *     one context are serialised by an internal lock, which is what lets the
+ *     Rust adapter present it as the `Fn` (not `FnMut`) closure
+ *     HostSettings::checksum requires.
  */
 #ifndef ENET_CRC_AMD_H
 #define ENET_CRC_AMD_H
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ENET_CRC_ABI_VERSION 2
+#define ENET_CRC_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define ENET_CRC_API __attribute__((visibility("default")))
@@ -56,6 +58,13 @@ typedef struct enet_crc_iov {
 
 typedef struct enet_crc_ctx enet_crc_ctx;
 
+/* Most entries in a context's device list. */
+#define ENET_CRC_MAX_LANES 64
+
+/* Per-call modes of enet_crc32_iov (enet_crc_ctx_set_percall_mode). */
+#define ENET_CRC_PERCALL_COPY 0     /* pinned staging -> H2D copy -> kernel -> D2H copy */
+#define ENET_CRC_PERCALL_ZEROCOPY 1 /* kernel reads mapped pinned memory, writes the result to it (default) */
+
 ENET_CRC_API int enet_crc_abi_version(void);
 ENET_CRC_API const char* enet_crc_strerror(int status);
 /* hipError_t of the last failing HIP call made by this thread (0 if none). */
@@ -63,10 +72,37 @@ ENET_CRC_API int enet_crc_last_hip_error(void);
 /* Number of visible HIP devices (0 when none), or a negative status. */
 ENET_CRC_API int enet_crc_device_count(void);
 
-/* Create a context bound to HIP device `device` (its own non-blocking stream,
- * pinned + device staging grown on demand). */
+/* Create a context bound to HIP device `device` (its own non-blocking streams,
+ * pinned + device staging grown on demand).  Same as
+ * enet_crc_ctx_create_multi(&device, 1, out_ctx). */
 ENET_CRC_API int enet_crc_ctx_create(int device, enet_crc_ctx** out_ctx);
+
+/*
+ * Create a context over a device list (the batch split across the
+ * GPUs of one node).  Entry i is a "lane": device devices[i] with its own stream
+ * pair, staging and (for i >= 1) host worker thread.  A device may appear more than
+ * once (two lanes on one GPU).  enet_crc32_ragged_host on such a context splits the
+ * batch into ndevices byte-balanced contiguous shards (enet_crc_shard_bounds) and
+ * checksums shard i on lane i, all lanes at once; the per-call and range-coder entry
+ * points use lane 0.  1 <= ndevices <= ENET_CRC_MAX_LANES.
+ */
+ENET_CRC_API int enet_crc_ctx_create_multi(const int* devices, uint32_t ndevices, enet_crc_ctx** out_ctx);
 ENET_CRC_API void enet_crc_ctx_destroy(enet_crc_ctx* ctx);
+/* Number of lanes (device-list entries) of a context, or ENET_CRC_E_INVALID. */
+ENET_CRC_API int enet_crc_ctx_lanes(const enet_crc_ctx* ctx);
+/* Select how enet_crc32_iov moves one datagram (ENET_CRC_PERCALL_*). */
+ENET_CRC_API int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode);
+
+/*
+ * Byte-balanced contiguous split of a batch into `nshards` packet ranges:
+ * bounds[0] = 0 <= bounds[1] <= ... <= bounds[nshards] = count; shard k is packets
+ * [bounds[k], bounds[k+1]).  Cut k is one past the first packet whose cumulative
+ * byte end reaches floor(total_bytes * k / nshards), so every shard is within one
+ * packet of total/nshards bytes.  lengths == NULL: an even split by packet count.
+ * Host function, no device work.
+ */
+ENET_CRC_API int enet_crc_shard_bounds(const uint32_t* lengths, uint64_t count, uint32_t nshards,
+                                       uint64_t* bounds);
 
 /*
  * Per-call drop-in for `crc32(in_buffers)` (src/crc32.rs:39-47).
@@ -74,7 +110,9 @@ ENET_CRC_API void enet_crc_ctx_destroy(enet_crc_ctx* ctx);
  * called at src/c/protocol.rs:1499 (one slice) and :2287 (up to 65 slices,
  * BUFFER_MAXIMUM, src/consts.rs:37).  Slices may be empty or NULL-with-len-0.
  * Gathers the slices into pinned staging, checksums on the GPU, writes the
- * reference value to *out_crc.  Synchronous.
+ * reference value to *out_crc.  Synchronous.  Zero-copy mode (the default): the
+ * kernel reads the gathered bytes from mapped pinned memory and writes the result
+ * to mapped memory, no copy-engine transfers (enet_crc_ctx_set_percall_mode).
  */
 ENET_CRC_API int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, uint32_t* out_crc);
 
@@ -94,10 +132,34 @@ ENET_CRC_API int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_
                              uint64_t count, uint32_t* d_out, void* hip_stream);
 
 /*
+ * Device-resident batch sharded over several devices: shard i is a uniform
+ * (d_offsets == NULL: packets at d_base + p*stride, `length` bytes) or ragged
+ * (d_offsets/d_lengths) batch in device `device`'s memory, checksummed on that
+ * device into d_out on hip_stream (a stream of that device, or NULL).  Every
+ * launch is asynchronous; the shards run concurrently on their devices.
+ */
+typedef struct enet_crc_shard {
+  int device;
+  const void* d_base;
+  const uint64_t* d_offsets; /* NULL: uniform shard */
+  const uint32_t* d_lengths;
+  uint64_t stride;
+  uint32_t length;
+  uint64_t count;
+  uint32_t* d_out;
+  void* hip_stream;
+} enet_crc_shard;
+
+ENET_CRC_API int enet_crc32_shards_device(const enet_crc_shard* shards, size_t nshards);
+
+/*
  * Host-resident ragged batch (the end-to-end path: host packet buffers such as
  * the UdpSocket receive buffers of src/c/protocol.rs:1660-1680 in, checksums
  * out).  Stages through pinned memory in chunks, overlapping copy and compute
- * on the context's stream pair.  Synchronous.
+ * on the context's stream pair.  On a multi-device context the batch is split into
+ * one byte-balanced shard per lane and the lanes run concurrently; outputs go to
+ * disjoint slices of h_out.  Synchronous.  On an error no later write into h_out
+ * happens (everything in flight is waited for first).
  */
 ENET_CRC_API int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t* h_offsets,
                            const uint32_t* h_lengths, uint64_t count, uint32_t* h_out);

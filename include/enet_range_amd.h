@@ -66,6 +66,39 @@ ENET_CRC_API int enet_range_decompress_ragged_device(const void* d_in, const uin
                                                      uint32_t* d_sizes, void* d_scratch, uint64_t scratch_bytes,
                                                      void* hip_stream);
 
+/*
+ * Host-memory drop-ins for the `Compressor` methods (src/compressor.rs:9-14, :36-69),
+ * on lane 0 of an enet_crc_ctx (the context owns the arenas and the staging).
+ *
+ * enet_range_compress_iov: `compress(&mut self, in_buffers, in_limit, out)`.  The
+ * slices are coded as the byte sequence compress.rs:103-126 reads (an empty slice
+ * after the first is one 0 byte, see above); in_limit == 0 or nbufs == 0 codes
+ * nothing (compress.rs:79).  *out_size = the reference's return value (0 = not
+ * coded within out_limit).  Only the first *out_size bytes of `out` are written.
+ *
+ * enet_range_decompress: `decompress(&mut self, in_data, out)`; *out_size = the
+ * reference's return value (0 = empty input or malformed stream, or out_limit
+ * reached).  Synchronous.
+ */
+ENET_CRC_API int enet_range_compress_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs,
+                                         size_t in_limit, uint8_t* out, size_t out_limit, size_t* out_size);
+ENET_CRC_API int enet_range_decompress(enet_crc_ctx* ctx, const uint8_t* in, size_t in_len, uint8_t* out,
+                                       size_t out_limit, size_t* out_size);
+
+/*
+ * Host-memory batches (a receive/send batch of datagrams in one launch): the same
+ * layout as the device entry points above, in host memory.  Only the first
+ * h_sizes[p] bytes of packet p's output window are written.  Synchronous.
+ */
+ENET_CRC_API int enet_range_compress_ragged_host(enet_crc_ctx* ctx, const void* h_in, const uint64_t* h_in_offsets,
+                                                 const uint32_t* h_in_lengths, uint64_t count, void* h_out,
+                                                 const uint64_t* h_out_offsets, const uint32_t* h_out_limits,
+                                                 uint32_t* h_sizes);
+ENET_CRC_API int enet_range_decompress_ragged_host(enet_crc_ctx* ctx, const void* h_in,
+                                                   const uint64_t* h_in_offsets, const uint32_t* h_in_lengths,
+                                                   uint64_t count, void* h_out, const uint64_t* h_out_offsets,
+                                                   const uint32_t* h_out_limits, uint32_t* h_sizes);
+
 #ifdef __cplusplus
 }
 #endif

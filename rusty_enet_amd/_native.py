@@ -62,7 +62,13 @@ _SIGNATURES = {
     "enet_crc_last_hip_error": (ctypes.c_int, []),
     "enet_crc_device_count": (ctypes.c_int, []),
     "enet_crc_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "enet_crc_ctx_create_multi": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_void_p)]),
     "enet_crc_ctx_destroy": (None, [ctypes.c_void_p]),
+    "enet_crc_ctx_lanes": (ctypes.c_int, [ctypes.c_void_p]),
+    "enet_crc_ctx_set_percall_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "enet_crc_shard_bounds": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
+    "enet_crc32_shards_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     "enet_crc32_iov": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Iov), ctypes.c_size_t, _u32p]),
     "enet_crc32_uniform_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
@@ -88,9 +94,28 @@ _SIGNATURES = {
                                           [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_void_p]),
     "enet_range_decompress_ragged_device": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_uint64] +
                                             [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_void_p]),
+    "enet_range_compress_iov": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Iov), ctypes.c_size_t, ctypes.c_size_t,
+                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "enet_range_decompress": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                             ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "enet_range_compress_ragged_host": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + [ctypes.c_void_p] * 4),
+    "enet_range_decompress_ragged_host": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_uint64] +
+                                          [ctypes.c_void_p] * 4),
 }
 
-ABI_VERSION = 2
+
+class Shard(ctypes.Structure):
+    """enet_crc_shard (include/enet_crc_amd.h)."""
+
+    _fields_ = [("device", ctypes.c_int), ("d_base", ctypes.c_void_p), ("d_offsets", ctypes.c_void_p),
+                ("d_lengths", ctypes.c_void_p), ("stride", ctypes.c_uint64), ("length", ctypes.c_uint32),
+                ("count", ctypes.c_uint64), ("d_out", ctypes.c_void_p), ("hip_stream", ctypes.c_void_p)]
+
+
+ENET_CRC_PERCALL_COPY = 0
+ENET_CRC_PERCALL_ZEROCOPY = 1
+
+ABI_VERSION = 3
 
 
 def lib() -> ctypes.CDLL:

@@ -34,17 +34,57 @@ def _as_u8(buf) -> np.ndarray:
     return np.frombuffer(buf, dtype=np.uint8)
 
 
+def _writable_u8(buf) -> np.ndarray:
+    """A writable uint8 view of ``buf`` (bytearray, memoryview, numpy array) without a copy."""
+    if isinstance(buf, np.ndarray):
+        if not buf.flags.c_contiguous or not buf.flags.writeable:
+            raise ValueError("out must be a writable contiguous array")
+        return buf.reshape(-1).view(np.uint8)
+    a = np.frombuffer(memoryview(buf).cast("B"), dtype=np.uint8)
+    if not a.flags.writeable:
+        raise ValueError("out must be writable")
+    return a
+
+
+def shard_bounds_native(lengths=None, count: Optional[int] = None, nshards: int = 1) -> np.ndarray:
+    """``enet_crc_shard_bounds``: the C++ byte-balanced split (nshards + 1 bounds)."""
+    if lengths is not None:
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        count = ln.size
+        ptr = ln.ctypes.data if ln.size else None
+    else:
+        ln, ptr = None, None
+    bounds = np.zeros(nshards + 1, dtype=np.uint64)
+    check(lib().enet_crc_shard_bounds(ptr, int(count or 0), nshards, bounds.ctypes.data), "enet_crc_shard_bounds")
+    return bounds
+
+
 class Context:
-    """Owns an ``enet_crc_ctx`` (stream + pinned/device staging) on one device.
+    """Owns an ``enet_crc_ctx`` (streams + pinned/device staging) on one device, or on a
+    device list (``devices=[0, 1, ...]``, duplicates allowed): host-memory batches are
+    then split into byte-balanced shards checksummed on all lanes at once.
 
     Calling the context is the per-call checksum hook: ``ctx([b"..", b".."])``.
     """
 
-    def __init__(self, device: int = 0):
-        self.device = device
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
+        devs = [int(d) for d in (devices if devices is not None else [device])]
+        if not devs:
+            raise ValueError("empty device list")
+        self.device = devs[0]
+        self.devices = devs
         handle = ctypes.c_void_p()
-        check(lib().enet_crc_ctx_create(device, ctypes.byref(handle)), "enet_crc_ctx_create")
+        arr = (ctypes.c_int * len(devs))(*devs)
+        check(lib().enet_crc_ctx_create_multi(arr, len(devs), ctypes.byref(handle)), "enet_crc_ctx_create_multi")
         self._handle = handle
+
+    @property
+    def lanes(self) -> int:
+        return lib().enet_crc_ctx_lanes(self._handle)
+
+    def set_percall_mode(self, mode: int) -> None:
+        """``_native.ENET_CRC_PERCALL_COPY`` or ``ENET_CRC_PERCALL_ZEROCOPY`` (default)."""
+        check(lib().enet_crc_ctx_set_percall_mode(self._handle, mode), "enet_crc_ctx_set_percall_mode")
 
     @property
     def handle(self) -> int:
@@ -93,6 +133,53 @@ class Context:
         check(lib().enet_crc32_ragged_host(self._handle, d.ctypes.data, off.ctypes.data, ln.ctypes.data,
                                            off.size, out.ctypes.data), "enet_crc32_ragged_host")
         return out
+
+    # range coder, host memory (src/compressor.rs:9-14) ---------------------
+    def range_compress(self, in_buffers: Sequence, in_limit: int, out) -> int:
+        """``Compressor::compress(in_buffers, in_limit, out)``: writes into ``out`` (a
+        writable buffer), returns the reference's size (0 = not coded)."""
+        arrays = [_as_u8(b) for b in in_buffers]
+        iovs = (Iov * max(1, len(arrays)))()
+        for i, a in enumerate(arrays):
+            iovs[i].data = a.ctypes.data if a.size else None
+            iovs[i].len = a.size
+        dst = _writable_u8(out)
+        size = ctypes.c_size_t()
+        check(lib().enet_range_compress_iov(self._handle, iovs, len(arrays), int(in_limit),
+                                            dst.ctypes.data if dst.size else None, dst.size, ctypes.byref(size)),
+              "enet_range_compress_iov")
+        return size.value
+
+    def range_decompress(self, in_data, out) -> int:
+        """``Compressor::decompress(in_data, out)``."""
+        src = _as_u8(in_data)
+        dst = _writable_u8(out)
+        size = ctypes.c_size_t()
+        check(lib().enet_range_decompress(self._handle, src.ctypes.data if src.size else None, src.size,
+                                          dst.ctypes.data if dst.size else None, dst.size, ctypes.byref(size)),
+              "enet_range_decompress")
+        return size.value
+
+    def range_ragged_host(self, decompress: bool, data, offsets, lengths, out_limits):
+        """Batch of packets in host memory; returns (out bytes, out offsets, sizes)."""
+        d = _as_u8(data)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        lim = np.ascontiguousarray(out_limits, dtype=np.uint32)
+        if not (off.shape == ln.shape == lim.shape):
+            raise ValueError("offsets, lengths and out_limits must have the same shape")
+        if off.size and int((off + ln).max()) > d.size:
+            raise ValueError("a packet extends past the end of data")
+        o_off = np.zeros(off.size, dtype=np.uint64)
+        if off.size > 1:
+            np.cumsum(lim[:-1], dtype=np.uint64, out=o_off[1:])
+        out = np.zeros(max(1, int(lim.sum(dtype=np.uint64))), dtype=np.uint8)
+        sizes = np.zeros(off.size, dtype=np.uint32)
+        fn = lib().enet_range_decompress_ragged_host if decompress else lib().enet_range_compress_ragged_host
+        check(fn(self._handle, d.ctypes.data, off.ctypes.data, ln.ctypes.data, off.size, out.ctypes.data,
+                 o_off.ctypes.data, lim.ctypes.data, sizes.ctypes.data),
+              "enet_range_decompress_ragged_host" if decompress else "enet_range_compress_ragged_host")
+        return out, o_off, sizes
 
 
 _default: dict[int, Context] = {}
@@ -144,31 +231,90 @@ def crc32_batch(data, *, offsets=None, lengths=None, stride: Optional[int] = Non
     """
     import torch
 
-    if not data.is_cuda or data.dtype != torch.uint8:
-        raise ValueError("data must be a uint8 CUDA/HIP tensor")
+    if not data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
+        raise ValueError("data must be a contiguous uint8 CUDA/HIP tensor")
+    dev = data.device
     if stream is None:
-        stream = torch.cuda.current_stream(data.device)
+        stream = torch.cuda.current_stream(dev)
+    elif stream.device != dev:
+        raise ValueError("stream must belong to the data's device")
     sptr = stream.cuda_stream
     if offsets is not None:
         if lengths is None:
             raise ValueError("ragged batch needs offsets and lengths")
-        if offsets.dtype not in (torch.int64, torch.uint64) or lengths.dtype not in (torch.int32, torch.uint32):
-            raise ValueError("offsets must be 64-bit, lengths 32-bit")
+        _check_dev(dev, offsets=(offsets, (torch.int64, torch.uint64)), lengths=(lengths, (torch.int32, torch.uint32)))
         n = offsets.numel()
+        if lengths.numel() != n:
+            raise ValueError("offsets and lengths must have one entry per packet")
         if out is None:
-            out = torch.empty(n, dtype=torch.int32, device=data.device)
-        crc32_ragged_device(data.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), n, out.data_ptr(), sptr)
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+        _check_dev(dev, out=(out, (torch.int32, torch.uint32)))
+        if out.numel() < n:
+            raise ValueError("out is too small")
+        with torch.cuda.device(dev):
+            crc32_ragged_device(data.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), n, out.data_ptr(), sptr)
         return out
     if stride is None or length is None:
         raise ValueError("uniform batch needs stride and length")
+    if stride < 0 or length < 0 or length > 0xFFFFFFFF:
+        raise ValueError("stride and length must be non-negative (length < 2**32)")
     if count is None:
-        count = (data.numel() - length) // stride + 1 if data.numel() >= length else 0
+        count = (data.numel() - length) // stride + 1 if data.numel() >= length and stride else 0
+    if count < 0:
+        raise ValueError("count must be non-negative")
     if count and (count - 1) * stride + length > data.numel():
         raise ValueError("batch extends past the end of data")
     if out is None:
-        out = torch.empty(count, dtype=torch.int32, device=data.device)
-    crc32_uniform_device(data.data_ptr(), stride, length, count, out.data_ptr(), sptr)
+        out = torch.empty(count, dtype=torch.int32, device=dev)
+    _check_dev(dev, out=(out, (torch.int32, torch.uint32)))
+    if out.numel() < count:
+        raise ValueError("out is too small")
+    with torch.cuda.device(dev):
+        crc32_uniform_device(data.data_ptr(), stride, length, count, out.data_ptr(), sptr)
     return out
+
+
+def _check_dev(dev, **tensors) -> None:
+    """Every tensor on `dev`, contiguous, with one of the allowed dtypes."""
+    for name, (t, dtypes) in tensors.items():
+        if not t.is_cuda or t.device != dev:
+            raise ValueError(f"{name} must be on {dev}")
+        if t.dtype not in dtypes:
+            raise ValueError(f"{name} must have dtype in {dtypes}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+
+
+def crc32_shards_device(shards: Sequence[dict]) -> None:
+    """``enet_crc32_shards_device``: one batch per device, launched on every device at
+    once.  Each shard is a dict with ``data`` (uint8 tensor) and either ``stride``/
+    ``length``/``count`` or ``offsets``/``lengths``, plus ``out`` (int32 tensor) and an
+    optional ``stream`` (torch stream of that device)."""
+    import torch
+
+    arr = (_native.Shard * max(1, len(shards)))()
+    for i, sh in enumerate(shards):
+        data, out = sh["data"], sh["out"]
+        dev = data.device
+        if not data.is_cuda or data.dtype != torch.uint8:
+            raise ValueError("data must be a uint8 device tensor")
+        _check_dev(dev, out=(out, (torch.int32, torch.uint32)))
+        stream = sh.get("stream") or torch.cuda.current_stream(dev)
+        arr[i].device = dev.index
+        arr[i].d_base = data.data_ptr()
+        arr[i].d_out = out.data_ptr()
+        arr[i].hip_stream = stream.cuda_stream
+        if "offsets" in sh:
+            off, ln = sh["offsets"], sh["lengths"]
+            _check_dev(dev, offsets=(off, (torch.int64, torch.uint64)), lengths=(ln, (torch.int32, torch.uint32)))
+            arr[i].d_offsets, arr[i].d_lengths, arr[i].count = off.data_ptr(), ln.data_ptr(), off.numel()
+        else:
+            arr[i].stride, arr[i].length, arr[i].count = sh["stride"], sh["length"], sh["count"]
+            if arr[i].count and (arr[i].count - 1) * arr[i].stride + arr[i].length > data.numel():
+                raise ValueError("shard extends past the end of its data")
+        if out.numel() < arr[i].count:
+            raise ValueError("out is too small")
+    check(lib().enet_crc32_shards_device(arr, len(shards)), "enet_crc32_shards_device")
 
 
 # checksum slot (SURVEY.md §8(b) batching semantics, §8(f)1-2) ------------------
@@ -186,14 +332,15 @@ def slot_adjust(crc: int, old_slot: int, new_slot: int, bytes_after_slot: int) -
 def _slot_batch_args(data, offsets, lengths, slot_offsets, slot_values):
     import torch
 
-    if not data.is_cuda or data.dtype != torch.uint8:
-        raise ValueError("data must be a uint8 CUDA/HIP tensor")
+    if not data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
+        raise ValueError("data must be a contiguous uint8 CUDA/HIP tensor")
     n = offsets.numel()
-    if offsets.dtype not in (torch.int64, torch.uint64):
-        raise ValueError("offsets must be 64-bit")
+    i32 = (torch.int32, torch.uint32)
+    _check_dev(data.device, offsets=(offsets, (torch.int64, torch.uint64)), lengths=(lengths, i32),
+               slot_offsets=(slot_offsets, i32), slot_values=(slot_values, i32))
     for name, t in (("lengths", lengths), ("slot_offsets", slot_offsets), ("slot_values", slot_values)):
-        if t.dtype not in (torch.int32, torch.uint32) or t.numel() != n or not t.is_cuda:
-            raise ValueError(f"{name} must be a 32-bit device tensor with one entry per datagram")
+        if t.numel() != n:
+            raise ValueError(f"{name} must have one entry per datagram")
     return n
 
 

@@ -1311,6 +1311,11 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   return L.streaming();
 }
 
+hipError_t launch_single(const uint8_t* base, uint32_t length, uint32_t* out, hipStream_t stream) {
+  Launcher<false> L{Batch<false>{(uint64_t)(uintptr_t)base, nullptr, nullptr, 0, length, 1}, out, stream, 1};
+  return L.streaming();
+}
+
 // Stream-ordered scratch for the ragged pre-pass comes from a pool of our own with an
 // unlimited release threshold: freed blocks stay cached, so the per-launch
 // hipMallocFromPoolAsync / hipFreeAsync pair costs no remapping (the default pool,

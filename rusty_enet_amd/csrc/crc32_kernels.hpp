@@ -10,6 +10,11 @@ namespace enet_crc {
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
                           uint32_t* out, hipStream_t stream);
 
+// One packet of `length` bytes at `base`, any memory the device can read (the per-call
+// path passes mapped pinned host memory), result to `out` (may be mapped host memory).
+// Register-staged loads only (no LDS-DMA from host memory).
+hipError_t launch_single(const uint8_t* base, uint32_t length, uint32_t* out, hipStream_t stream);
+
 // Packets p at base + offsets[p], lengths[p] bytes (device arrays).
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
                          uint64_t count, uint32_t* out, hipStream_t stream);

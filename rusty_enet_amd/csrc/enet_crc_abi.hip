@@ -1,25 +1,36 @@
-// C ABI of the MI355X CRC-32 path (include/enet_crc_amd.h).
+// C ABI of the MI355X CRC-32 path (include/enet_crc_amd.h, include/enet_range_amd.h).
 //
 // The reference hook is a synchronous `Fn(&[&[u8]]) -> u32` called on the
 // thread running Host::service()/flush() (src/host.rs:185-201, src/c/protocol.rs
 // :1499 and :2287).  This file maps that surface and the batch entry points
-// onto the gfx950 kernels in crc32_kernels.hip.  There is no CPU path: every
-// checksum comes from the GPU or the call returns an error.
+// onto the gfx950 kernels in crc32_kernels.hip / range_coder.hip.  There is no
+// CPU path: every checksum comes from the GPU or the call returns an error.
+//
+// A context owns one "lane" per entry of its device list (duplicates allowed):
+// a pair of pinned/device staging slots with their streams, and the range-coder
+// staging.  Host-memory batches are split into byte-balanced contiguous shards,
+// one per lane; lane 0 runs on the calling thread, the others on the context's
+// worker threads (one per extra lane), each on its own device and streams.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/enet_crc_amd.h"
+#include "../../include/enet_range_amd.h"
 #include "crc32_kernels.hpp"
 #include "crc32_slot.hpp"
 #include "range_coder.hpp"
-#include "../../include/enet_range_amd.h"
 
 namespace enet_crc {
 
@@ -34,10 +45,16 @@ int fail_hip(hipError_t e) {
   return ENET_CRC_E_HIP;
 }
 
-#define ENET_HIP_TRY(expr)                 \
-  do {                                     \
-    hipError_t _e = (expr);                \
+#define ENET_HIP_TRY(expr)                     \
+  do {                                         \
+    hipError_t _e = (expr);                    \
     if (_e != hipSuccess) return fail_hip(_e); \
+  } while (0)
+
+#define ENET_TRY(expr)              \
+  do {                              \
+    int _s = (expr);                \
+    if (_s != ENET_CRC_OK) return _s; \
   } while (0)
 
 constexpr int kMaxDevices = 64;
@@ -48,13 +65,21 @@ struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
+    if (dev >= 0 && prev != dev) (void)hipSetDevice(dev);
   }
   ~DeviceGuard() {
     int cur = -1;
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+// Device of an explicit stream (-1 for the legacy default stream / an unknown one):
+// the device entry points launch on the stream's device, whatever device is current.
+int stream_device(hipStream_t s) {
+  if (s == nullptr) return -1;
+  int d = -1;
+  return hipStreamGetDevice(s, &d) == hipSuccess ? d : -1;
+}
 
 }  // namespace
 
@@ -104,34 +129,176 @@ int cu_count_for_current_device() {
   return n;
 }
 
+// Byte-balanced contiguous split (the same cut points as rusty_enet_amd/shards.py
+// shard_bounds): cut k is one past the first packet whose cumulative byte end reaches
+// floor(total * k / n).  lengths == NULL: an even split of `count` packets.
+void split_bounds(const uint32_t* lengths, uint64_t count, uint32_t n, uint64_t* b) {
+  b[0] = 0;
+  b[n] = count;
+  if (!lengths) {
+    for (uint32_t k = 1; k < n; ++k) b[k] = (uint64_t)((unsigned __int128)count * k / n);
+    return;
+  }
+  unsigned __int128 total = 0;
+  for (uint64_t i = 0; i < count; ++i) total += lengths[i];
+  uint64_t i = 0;
+  unsigned __int128 end = count ? lengths[0] : 0;  // byte end of packet i
+  for (uint32_t k = 1; k < n; ++k) {
+    const unsigned __int128 target = total * k / n;
+    if (target == 0 || count == 0) {
+      b[k] = 0;
+      continue;
+    }
+    while (end < target && i + 1 < count) end += lengths[++i];
+    b[k] = i + 1;
+  }
+}
+
 }  // namespace enet_crc
 
 using namespace enet_crc;
 
+namespace {
+
+// Pinned host buffer + device mirror of `T`, grown on demand (contents not kept).
+template <typename T>
+struct Mirror {
+  T* h = nullptr;
+  T* d = nullptr;
+  size_t cap = 0;  // elements
+  int grow(size_t n, size_t pad_bytes = 0) {
+    if (n <= cap && h) return ENET_CRC_OK;
+    release();
+    n = std::max<size_t>(n, 64);
+    const size_t bytes = (n * sizeof(T) + pad_bytes + 15) & ~(size_t)15;
+    ENET_HIP_TRY(hipHostMalloc((void**)&h, bytes, hipHostMallocDefault));
+    ENET_HIP_TRY(hipMalloc((void**)&d, bytes));
+    cap = n;
+    return ENET_CRC_OK;
+  }
+  void release() {
+    if (h) (void)hipHostFree(h);
+    if (d) (void)hipFree(d);
+    h = nullptr;
+    d = nullptr;
+    cap = 0;
+  }
+};
+
 // One pipeline slot of the host path: pinned input bytes + descriptors, device
 // copies, pinned output.
 struct StageSlot {
-  uint8_t* h_bytes = nullptr;
-  uint64_t* h_offsets = nullptr;
-  uint32_t* h_lengths = nullptr;
-  uint32_t* h_out = nullptr;
-  uint8_t* d_bytes = nullptr;
-  uint64_t* d_offsets = nullptr;
-  uint32_t* d_lengths = nullptr;
-  uint32_t* d_out = nullptr;
-  size_t byte_cap = 0;
-  size_t pkt_cap = 0;
+  Mirror<uint8_t> bytes;  // +16 B: the kernels' 4-byte-grid loads stay inside whole 16-B lines
+  Mirror<uint64_t> offsets;
+  Mirror<uint32_t> lengths;
+  Mirror<uint32_t> out;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   uint64_t first = 0;  // packet range staged in this slot
   uint64_t n = 0;
   bool busy = false;
+  void release() {
+    bytes.release();
+    offsets.release();
+    lengths.release();
+    out.release();
+  }
 };
 
-struct enet_crc_ctx {
+// Range-coder staging of a lane (host-memory compress/decompress entry points).
+struct RangeStage {
+  Mirror<uint8_t> in, out;
+  Mirror<uint64_t> in_off, out_off;
+  Mirror<uint32_t> in_len, out_lim, sizes;
+  void* d_scratch = nullptr;
+  uint64_t workers = 0;
+  void release() {
+    in.release();
+    out.release();
+    in_off.release();
+    out_off.release();
+    in_len.release();
+    out_lim.release();
+    sizes.release();
+    if (d_scratch) (void)hipFree(d_scratch);
+    d_scratch = nullptr;
+    workers = 0;
+  }
+};
+
+// Per-call (enet_crc32_iov) buffers: a pinned, device-mapped input buffer the kernel
+// reads directly (zero-copy mode) and a mapped result word.
+struct PerCall {
+  uint8_t* h_in = nullptr;
+  size_t cap = 0;
+  uint32_t* h_res = nullptr;  // [0] = checksum (mapped: written by the kernel)
+};
+
+// A worker thread bound to one lane: runs one job at a time for the calling thread.
+class Worker {
+ public:
+  Worker() : th_([this] { loop(); }) {}
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void start(std::function<int()> job) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = std::move(job);
+      has_job_ = true;
+      done_ = false;
+    }
+    cv_.notify_all();
+  }
+  int wait() {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [this] { return done_; });
+    return result_;
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [this] { return has_job_ || quit_; });
+      if (quit_) return;
+      std::function<int()> job = std::move(job_);
+      has_job_ = false;
+      g.unlock();
+      const int r = job();
+      g.lock();
+      result_ = r;
+      done_ = true;
+      cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::function<int()> job_;
+  bool has_job_ = false, done_ = true, quit_ = false;
+  int result_ = ENET_CRC_OK;
+  std::thread th_;
+};
+
+struct Lane {
   int device = 0;
-  std::mutex lock;
   StageSlot slot[2];
+  RangeStage range;
+  std::unique_ptr<Worker> worker;  // lanes >= 1
+};
+
+}  // namespace
+
+struct enet_crc_ctx {
+  std::mutex lock;
+  std::vector<Lane> lanes;
+  PerCall call;
+  int percall_mode = ENET_CRC_PERCALL_ZEROCOPY;
 };
 
 // One slot of a pinned receive ring (include/enet_crc_amd.h).
@@ -159,59 +326,126 @@ struct enet_crc_ring {
 
 namespace {
 
-void free_slot_buffers(StageSlot& s) {
-  if (s.h_bytes) (void)hipHostFree(s.h_bytes);
-  if (s.h_offsets) (void)hipHostFree(s.h_offsets);
-  if (s.h_lengths) (void)hipHostFree(s.h_lengths);
-  if (s.h_out) (void)hipHostFree(s.h_out);
-  if (s.d_bytes) (void)hipFree(s.d_bytes);
-  if (s.d_offsets) (void)hipFree(s.d_offsets);
-  if (s.d_lengths) (void)hipFree(s.d_lengths);
-  if (s.d_out) (void)hipFree(s.d_out);
-  s.h_bytes = nullptr; s.h_offsets = nullptr; s.h_lengths = nullptr; s.h_out = nullptr;
-  s.d_bytes = nullptr; s.d_offsets = nullptr; s.d_lengths = nullptr; s.d_out = nullptr;
-  s.byte_cap = 0; s.pkt_cap = 0;
-}
-
-// Grows the slot to hold `bytes` input bytes and `pkts` packets (caller holds the ctx lock,
-// the slot is idle).
-int reserve_slot(StageSlot& s, size_t bytes, size_t pkts) {
-  bytes = std::max<size_t>(bytes, 4096);
-  pkts = std::max<size_t>(pkts, 64);
-  if (bytes > s.byte_cap) {
-    if (s.h_bytes) (void)hipHostFree(s.h_bytes);
-    if (s.d_bytes) (void)hipFree(s.d_bytes);
-    s.h_bytes = nullptr; s.d_bytes = nullptr; s.byte_cap = 0;
-    // +16: the kernel's 4-byte-grid loads never cross the packet's own words,
-    // but keep the staging allocation a whole number of 16-byte lines.
-    const size_t alloc = (bytes + 16 + 15) & ~(size_t)15;
-    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_bytes, alloc, hipHostMallocDefault));
-    ENET_HIP_TRY(hipMalloc((void**)&s.d_bytes, alloc));
-    s.byte_cap = bytes;
-  }
-  if (pkts > s.pkt_cap) {
-    if (s.h_offsets) (void)hipHostFree(s.h_offsets);
-    if (s.h_lengths) (void)hipHostFree(s.h_lengths);
-    if (s.h_out) (void)hipHostFree(s.h_out);
-    if (s.d_offsets) (void)hipFree(s.d_offsets);
-    if (s.d_lengths) (void)hipFree(s.d_lengths);
-    if (s.d_out) (void)hipFree(s.d_out);
-    s.h_offsets = nullptr; s.h_lengths = nullptr; s.h_out = nullptr;
-    s.d_offsets = nullptr; s.d_lengths = nullptr; s.d_out = nullptr; s.pkt_cap = 0;
-    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_offsets, pkts * sizeof(uint64_t), hipHostMallocDefault));
-    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_lengths, pkts * sizeof(uint32_t), hipHostMallocDefault));
-    ENET_HIP_TRY(hipHostMalloc((void**)&s.h_out, pkts * sizeof(uint32_t), hipHostMallocDefault));
-    ENET_HIP_TRY(hipMalloc((void**)&s.d_offsets, pkts * sizeof(uint64_t)));
-    ENET_HIP_TRY(hipMalloc((void**)&s.d_lengths, pkts * sizeof(uint32_t)));
-    ENET_HIP_TRY(hipMalloc((void**)&s.d_out, pkts * sizeof(uint32_t)));
-    s.pkt_cap = pkts;
-  }
-  return ENET_CRC_OK;
-}
-
 // Host path chunking: at most this many staged bytes / packets per slot.
 constexpr size_t kStageBytes = 64u << 20;
 constexpr size_t kStagePackets = 1u << 18;
+// Concurrent coders of a host-memory range-coder batch (scratch: workers x 64 KiB).
+constexpr uint64_t kRangeHostWorkers = 16384;
+
+// Fault injection for the error-path tests (tests/test_gpu_multi.py): the k-th chunk
+// (1-based) of every enet_crc32_ragged_host shard fails as if its staging allocation had.
+int injected_stage_fault() {
+  const char* v = getenv("ENET_CRC_INJECT_STAGE_FAULT");
+  return v ? atoi(v) : 0;
+}
+
+// Waits for whatever the lane's slots still have in flight and forgets it (error exits:
+// no copy-out into the caller's buffers, no buffer reuse under a running copy).
+void quiesce(Lane& L) {
+  for (auto& s : L.slot) {
+    if (s.busy && s.stream) (void)hipStreamSynchronize(s.stream);
+    s.busy = false;
+  }
+}
+
+// Packets [0, count) of one shard, on lane L's device: chunks of <= 64 MiB / 256K
+// packets alternate between the two staging slots, so the H2D copy of chunk i+1
+// overlaps the kernel of chunk i.  Caller holds the context lock.
+int ragged_host_shard(Lane& L, const uint8_t* base, const uint64_t* h_offsets, const uint32_t* h_lengths,
+                      uint64_t count, uint32_t* h_out) {
+  if (count == 0) return ENET_CRC_OK;
+  DeviceGuard g(L.device);
+  struct Quiesce {
+    Lane& L;
+    bool armed = true;
+    ~Quiesce() {
+      if (armed) quiesce(L);
+    }
+  } guard{L};
+  const int fault_at = injected_stage_fault();
+
+  // Drain a slot: wait for its kernel + D2H, copy checksums out.
+  auto drain = [&](StageSlot& s) -> int {
+    if (!s.busy) return ENET_CRC_OK;
+    ENET_HIP_TRY(hipEventSynchronize(s.done));
+    memcpy(h_out + s.first, s.out.h, s.n * sizeof(uint32_t));
+    s.busy = false;
+    return ENET_CRC_OK;
+  };
+
+  uint64_t p = 0;
+  int which = 0, chunk = 0;
+  while (p < count) {
+    StageSlot& s = L.slot[which];
+    ENET_TRY(drain(s));
+    // Chunk [p, q): packets whose byte span [lo, hi) fits the staging size.
+    uint64_t lo = h_offsets[p], hi = h_offsets[p] + h_lengths[p];
+    uint64_t q = p + 1;
+    while (q < count && q - p < kStagePackets) {
+      const uint64_t nlo = std::min<uint64_t>(lo, h_offsets[q]);
+      const uint64_t nhi = std::max<uint64_t>(hi, h_offsets[q] + h_lengths[q]);
+      if (nhi - nlo > kStageBytes) break;
+      lo = nlo;
+      hi = nhi;
+      ++q;
+    }
+    if (++chunk == fault_at) return ENET_CRC_E_NOMEM;
+    // Keep the device copy at the same offset mod 4 as the host bytes, so the
+    // kernel sees the same word grid (not required for correctness).
+    const uint64_t lo_al = lo & ~(uint64_t)3;
+    const size_t span = (size_t)(hi - lo_al);
+    const size_t n = (size_t)(q - p);
+    ENET_TRY(s.bytes.grow(std::max<size_t>(span, 4096), 16));
+    ENET_TRY(s.offsets.grow(n));
+    ENET_TRY(s.lengths.grow(n));
+    ENET_TRY(s.out.grow(n));
+    memcpy(s.bytes.h, base + lo_al, span);
+    for (uint64_t i = p; i < q; ++i) {
+      s.offsets.h[i - p] = h_offsets[i] - lo_al;
+      s.lengths.h[i - p] = h_lengths[i];
+    }
+    s.first = p;
+    s.n = n;
+    s.busy = true;  // from here on the slot's stream may hold work: quiesce() waits for it
+    ENET_HIP_TRY(hipMemcpyAsync(s.bytes.d, s.bytes.h, span, hipMemcpyHostToDevice, s.stream));
+    ENET_HIP_TRY(hipMemcpyAsync(s.offsets.d, s.offsets.h, n * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream));
+    ENET_HIP_TRY(hipMemcpyAsync(s.lengths.d, s.lengths.h, n * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
+    ENET_HIP_TRY(launch_ragged(s.bytes.d, s.offsets.d, s.lengths.d, n, s.out.d, s.stream));
+    ENET_HIP_TRY(hipMemcpyAsync(s.out.h, s.out.d, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+    ENET_HIP_TRY(hipEventRecord(s.done, s.stream));
+    p = q;
+    which ^= 1;
+  }
+  for (auto& s : L.slot) ENET_TRY(drain(s));
+  guard.armed = false;
+  return ENET_CRC_OK;
+}
+
+void destroy_lane(Lane& L) {
+  L.worker.reset();  // joins the thread first: no job can still be using the buffers
+  DeviceGuard g(L.device);
+  for (auto& s : L.slot) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    s.release();
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s.stream = nullptr;
+    s.done = nullptr;
+  }
+  L.range.release();
+}
+
+// Runs job(lane index) on every lane: lane 0 on this thread, the others on their
+// workers; returns the first non-OK status (all lanes have finished by then).
+int run_on_lanes(enet_crc_ctx* ctx, uint32_t nlanes, const std::function<int(uint32_t)>& job) {
+  for (uint32_t i = 1; i < nlanes; ++i) ctx->lanes[i].worker->start([&job, i] { return job(i); });
+  int st = job(0);
+  for (uint32_t i = 1; i < nlanes; ++i) {
+    const int r = ctx->lanes[i].worker->wait();
+    if (st == ENET_CRC_OK) st = r;
+  }
+  return st;
+}
 
 }  // namespace
 
@@ -240,39 +474,64 @@ int enet_crc_device_count(void) {
   return n;
 }
 
-int enet_crc_ctx_create(int device, enet_crc_ctx** out_ctx) {
+int enet_crc_shard_bounds(const uint32_t* lengths, uint64_t count, uint32_t nshards, uint64_t* bounds) {
+  if (nshards == 0 || !bounds) return ENET_CRC_E_INVALID;
+  split_bounds(lengths, count, nshards, bounds);
+  return ENET_CRC_OK;
+}
+
+int enet_crc_ctx_create_multi(const int* devices, uint32_t ndevices, enet_crc_ctx** out_ctx) {
   if (!out_ctx) return ENET_CRC_E_INVALID;
   *out_ctx = nullptr;
+  if (!devices || ndevices == 0 || ndevices > ENET_CRC_MAX_LANES) return ENET_CRC_E_INVALID;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n <= 0) return e == hipSuccess ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
-  if (device < 0 || device >= n) return ENET_CRC_E_NO_DEVICE;
+  if (e != hipSuccess || n <= 0) return e == hipSuccess || e == hipErrorNoDevice ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
+  for (uint32_t i = 0; i < ndevices; ++i)
+    if (devices[i] < 0 || devices[i] >= n) return ENET_CRC_E_NO_DEVICE;
   enet_crc_ctx* ctx = new (std::nothrow) enet_crc_ctx();
   if (!ctx) return ENET_CRC_E_NOMEM;
-  ctx->device = device;
-  DeviceGuard g(device);
-  for (auto& s : ctx->slot) {
-    hipError_t se = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-    if (se == hipSuccess) se = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
-    if (se != hipSuccess) {
+  ctx->lanes.resize(ndevices);
+  for (uint32_t i = 0; i < ndevices; ++i) {
+    Lane& L = ctx->lanes[i];
+    L.device = devices[i];
+    DeviceGuard g(L.device);
+    for (auto& s : L.slot) {
+      hipError_t se = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+      if (se == hipSuccess) se = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+      if (se != hipSuccess) {
+        enet_crc_ctx_destroy(ctx);
+        return fail_hip(se);
+      }
+    }
+    if (i > 0) L.worker.reset(new (std::nothrow) Worker());
+    if (i > 0 && !L.worker) {
       enet_crc_ctx_destroy(ctx);
-      return fail_hip(se);
+      return ENET_CRC_E_NOMEM;
     }
   }
   *out_ctx = ctx;
   return ENET_CRC_OK;
 }
 
+int enet_crc_ctx_create(int device, enet_crc_ctx** out_ctx) { return enet_crc_ctx_create_multi(&device, 1, out_ctx); }
+
+int enet_crc_ctx_lanes(const enet_crc_ctx* ctx) { return ctx ? (int)ctx->lanes.size() : ENET_CRC_E_INVALID; }
+
+int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode) {
+  if (!ctx || (mode != ENET_CRC_PERCALL_COPY && mode != ENET_CRC_PERCALL_ZEROCOPY)) return ENET_CRC_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  ctx->percall_mode = mode;
+  return ENET_CRC_OK;
+}
+
 void enet_crc_ctx_destroy(enet_crc_ctx* ctx) {
   if (!ctx) return;
-  {
-    DeviceGuard g(ctx->device);
-    for (auto& s : ctx->slot) {
-      if (s.stream) (void)hipStreamSynchronize(s.stream);
-      free_slot_buffers(s);
-      if (s.done) (void)hipEventDestroy(s.done);
-      if (s.stream) (void)hipStreamDestroy(s.stream);
-    }
+  for (auto& L : ctx->lanes) destroy_lane(L);
+  if (!ctx->lanes.empty()) {
+    DeviceGuard g(ctx->lanes[0].device);
+    if (ctx->call.h_in) (void)hipHostFree(ctx->call.h_in);
+    if (ctx->call.h_res) (void)hipHostFree(ctx->call.h_res);
   }
   delete ctx;
 }
@@ -281,8 +540,9 @@ int enet_crc32_uniform_device(const void* d_base, uint64_t stride, uint32_t leng
                               uint32_t* d_out, void* hip_stream) {
   if (count == 0) return ENET_CRC_OK;
   if (!d_out || (!d_base && length > 0)) return ENET_CRC_E_INVALID;
-  hipError_t e = launch_uniform(static_cast<const uint8_t*>(d_base), stride, length, count, d_out,
-                                static_cast<hipStream_t>(hip_stream));
+  const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  DeviceGuard g(stream_device(stream));
+  hipError_t e = launch_uniform(static_cast<const uint8_t*>(d_base), stride, length, count, d_out, stream);
   return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
 }
 
@@ -290,9 +550,30 @@ int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_offsets, cons
                              uint64_t count, uint32_t* d_out, void* hip_stream) {
   if (count == 0) return ENET_CRC_OK;
   if (!d_base || !d_offsets || !d_lengths || !d_out) return ENET_CRC_E_INVALID;
-  hipError_t e = launch_ragged(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, d_out,
-                               static_cast<hipStream_t>(hip_stream));
+  const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  DeviceGuard g(stream_device(stream));
+  hipError_t e = launch_ragged(static_cast<const uint8_t*>(d_base), d_offsets, d_lengths, count, d_out, stream);
   return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+}
+
+int enet_crc32_shards_device(const enet_crc_shard* shards, size_t nshards) {
+  if (nshards > 0 && !shards) return ENET_CRC_E_INVALID;
+  for (size_t i = 0; i < nshards; ++i) {
+    const enet_crc_shard& s = shards[i];
+    if (s.count == 0) continue;
+    if (!s.d_out || !s.d_base || (s.d_offsets != nullptr) != (s.d_lengths != nullptr)) return ENET_CRC_E_INVALID;
+  }
+  for (size_t i = 0; i < nshards; ++i) {
+    const enet_crc_shard& s = shards[i];
+    if (s.count == 0) continue;
+    DeviceGuard g(s.device);
+    const hipStream_t stream = static_cast<hipStream_t>(s.hip_stream);
+    const uint8_t* base = static_cast<const uint8_t*>(s.d_base);
+    const hipError_t e = s.d_offsets ? launch_ragged(base, s.d_offsets, s.d_lengths, s.count, s.d_out, stream)
+                                     : launch_uniform(base, s.stride, s.length, s.count, s.d_out, stream);
+    if (e != hipSuccess) return fail_hip(e);
+  }
+  return ENET_CRC_OK;
 }
 
 // Shared body of the batched verify / insert entry points: checksum the datagrams as
@@ -304,6 +585,7 @@ static int slot_batch(bool insert, uint8_t* d_base, const uint64_t* d_offsets, c
   if (!d_base || !d_offsets || !d_lengths || !d_slot_offsets || !d_slot_values || !d_crc || (!insert && !d_ok))
     return ENET_CRC_E_INVALID;
   const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  DeviceGuard g(stream_device(stream));
   const uint32_t* ladder = nullptr;
   ENET_HIP_TRY(device_slot_ladder(&ladder));
   ENET_HIP_TRY(launch_ragged(d_base, d_offsets, d_lengths, count, d_crc, stream));
@@ -341,20 +623,51 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
   }
   if (total > 0xFFFFFFFFull) return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
-  DeviceGuard g(ctx->device);
-  StageSlot& s = ctx->slot[0];
-  int st = reserve_slot(s, total, 1);
-  if (st != ENET_CRC_OK) return st;
+  Lane& L = ctx->lanes[0];
+  DeviceGuard g(L.device);
+  StageSlot& s = L.slot[0];
+  quiesce(L);  // nothing of an earlier (failed) call may still use the buffers
+  if (ctx->percall_mode == ENET_CRC_PERCALL_ZEROCOPY) {
+    // The kernel reads the gathered bytes straight from pinned host memory and writes
+    // the checksum into mapped host memory: no copy engine on the path.
+    PerCall& c = ctx->call;
+    if (total + 16 > c.cap || !c.h_in) {
+      if (c.h_in) (void)hipHostFree(c.h_in);
+      c.h_in = nullptr;
+      c.cap = 0;
+      const size_t cap = std::max<size_t>((total + 16 + 4095) & ~(size_t)4095, 8192);
+      ENET_HIP_TRY(hipHostMalloc((void**)&c.h_in, cap, hipHostMallocMapped));
+      c.cap = cap;
+    }
+    if (!c.h_res) ENET_HIP_TRY(hipHostMalloc((void**)&c.h_res, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    size_t pos = 0;  // concatenation, src/crc32.rs:41-42
+    for (size_t i = 0; i < nbufs; ++i) {
+      if (bufs[i].len) memcpy(c.h_in + pos, bufs[i].data, bufs[i].len);
+      pos += bufs[i].len;
+    }
+    uint8_t* d_in = nullptr;
+    uint32_t* d_res = nullptr;
+    ENET_HIP_TRY(hipHostGetDevicePointer((void**)&d_in, c.h_in, 0));
+    ENET_HIP_TRY(hipHostGetDevicePointer((void**)&d_res, c.h_res, 0));
+    ENET_HIP_TRY(launch_single(d_in, (uint32_t)total, d_res, s.stream));
+    ENET_HIP_TRY(hipStreamSynchronize(s.stream));
+    *out_crc = __atomic_load_n(&c.h_res[0], __ATOMIC_ACQUIRE);
+    return ENET_CRC_OK;
+  }
+  ENET_TRY(s.bytes.grow(std::max<size_t>(total, 4096), 16));
+  ENET_TRY(s.out.grow(1));
   size_t pos = 0;  // concatenation, src/crc32.rs:41-42
   for (size_t i = 0; i < nbufs; ++i) {
-    if (bufs[i].len) memcpy(s.h_bytes + pos, bufs[i].data, bufs[i].len);
+    if (bufs[i].len) memcpy(s.bytes.h + pos, bufs[i].data, bufs[i].len);
     pos += bufs[i].len;
   }
-  if (total) ENET_HIP_TRY(hipMemcpyAsync(s.d_bytes, s.h_bytes, total, hipMemcpyHostToDevice, s.stream));
-  ENET_HIP_TRY(launch_uniform(s.d_bytes, 0, (uint32_t)total, 1, s.d_out, s.stream));
-  ENET_HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+  s.busy = true;
+  if (total) ENET_HIP_TRY(hipMemcpyAsync(s.bytes.d, s.bytes.h, total, hipMemcpyHostToDevice, s.stream));
+  ENET_HIP_TRY(launch_uniform(s.bytes.d, 0, (uint32_t)total, 1, s.out.d, s.stream));
+  ENET_HIP_TRY(hipMemcpyAsync(s.out.h, s.out.d, sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
   ENET_HIP_TRY(hipStreamSynchronize(s.stream));
-  *out_crc = s.h_out[0];
+  s.busy = false;
+  *out_crc = s.out.h[0];
   return ENET_CRC_OK;
 }
 
@@ -364,62 +677,14 @@ int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t
   if (count == 0) return ENET_CRC_OK;
   if (!h_base || !h_offsets || !h_lengths || !h_out) return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
-  DeviceGuard g(ctx->device);
   const uint8_t* base = static_cast<const uint8_t*>(h_base);
-
-  // Drain a slot: wait for its kernel + D2H, copy checksums out.
-  auto drain = [&](StageSlot& s) -> int {
-    if (!s.busy) return ENET_CRC_OK;
-    ENET_HIP_TRY(hipEventSynchronize(s.done));
-    memcpy(h_out + s.first, s.h_out, s.n * sizeof(uint32_t));
-    s.busy = false;
-    return ENET_CRC_OK;
-  };
-
-  uint64_t p = 0;
-  int which = 0;
-  while (p < count) {
-    StageSlot& s = ctx->slot[which];
-    int st = drain(s);
-    if (st != ENET_CRC_OK) return st;
-    // Chunk [p, q): packets whose byte span [lo, hi) fits the staging size.
-    uint64_t lo = h_offsets[p], hi = h_offsets[p] + h_lengths[p];
-    uint64_t q = p + 1;
-    while (q < count && q - p < kStagePackets) {
-      const uint64_t nlo = std::min<uint64_t>(lo, h_offsets[q]);
-      const uint64_t nhi = std::max<uint64_t>(hi, h_offsets[q] + h_lengths[q]);
-      if (nhi - nlo > kStageBytes) break;
-      lo = nlo; hi = nhi; ++q;
-    }
-    // Keep the device copy at the same offset mod 4 as the host bytes, so the
-    // kernel sees the same word grid (not required for correctness).
-    const uint64_t lo_al = lo & ~(uint64_t)3;
-    const size_t span = (size_t)(hi - lo_al);
-    st = reserve_slot(s, span, (size_t)(q - p));
-    if (st != ENET_CRC_OK) return st;
-    memcpy(s.h_bytes, base + lo_al, span);
-    for (uint64_t i = p; i < q; ++i) {
-      s.h_offsets[i - p] = h_offsets[i] - lo_al;
-      s.h_lengths[i - p] = h_lengths[i];
-    }
-    const size_t n = (size_t)(q - p);
-    ENET_HIP_TRY(hipMemcpyAsync(s.d_bytes, s.h_bytes, span, hipMemcpyHostToDevice, s.stream));
-    ENET_HIP_TRY(hipMemcpyAsync(s.d_offsets, s.h_offsets, n * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream));
-    ENET_HIP_TRY(hipMemcpyAsync(s.d_lengths, s.h_lengths, n * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
-    ENET_HIP_TRY(launch_ragged(s.d_bytes, s.d_offsets, s.d_lengths, n, s.d_out, s.stream));
-    ENET_HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
-    ENET_HIP_TRY(hipEventRecord(s.done, s.stream));
-    s.first = p;
-    s.n = n;
-    s.busy = true;
-    p = q;
-    which ^= 1;
-  }
-  for (auto& s : ctx->slot) {
-    int st = drain(s);
-    if (st != ENET_CRC_OK) return st;
-  }
-  return ENET_CRC_OK;
+  const uint32_t nl = (uint32_t)std::min<uint64_t>(ctx->lanes.size(), count);
+  if (nl <= 1) return ragged_host_shard(ctx->lanes[0], base, h_offsets, h_lengths, count, h_out);
+  std::vector<uint64_t> b(nl + 1);
+  split_bounds(h_lengths, count, nl, b.data());
+  return run_on_lanes(ctx, nl, [&](uint32_t i) {
+    return ragged_host_shard(ctx->lanes[i], base, h_offsets + b[i], h_lengths + b[i], b[i + 1] - b[i], h_out + b[i]);
+  });
 }
 
 static void ring_free_slot(RingSlot& s) {
@@ -444,7 +709,7 @@ int enet_crc_ring_create(int device, uint32_t nslots, uint64_t slot_bytes, uint3
   if (nslots == 0 || nslots > 64 || slot_bytes == 0 || slot_packets == 0) return ENET_CRC_E_INVALID;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n <= 0) return e == hipSuccess ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
+  if (e != hipSuccess || n <= 0) return e == hipSuccess || e == hipErrorNoDevice ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
   if (device < 0 || device >= n) return ENET_CRC_E_NO_DEVICE;
   enet_crc_ring* r = new (std::nothrow) enet_crc_ring();
   if (!r) return ENET_CRC_E_NOMEM;
@@ -497,23 +762,22 @@ int enet_crc_ring_slot(enet_crc_ring* r, uint32_t slot, uint8_t** data, uint64_t
 int enet_crc_ring_submit(enet_crc_ring* r, uint32_t slot, uint64_t count) {
   if (!r || slot >= r->slots.size() || count > r->slot_packets) return ENET_CRC_E_INVALID;
   RingSlot& s = r->slots[slot];
-  uint64_t span = 0;  // bytes [0, span) of the slot hold every packet
-  for (uint64_t i = 0; i < count; ++i) {
-    const uint64_t o = s.h_offsets[i], l = s.h_lengths[i];
-    if (o > r->slot_bytes || l > r->slot_bytes - o) return ENET_CRC_E_INVALID;
-    span = std::max(span, o + l);
-  }
   {
     std::lock_guard<std::mutex> lk(r->lock);
     if (s.busy) return ENET_CRC_E_INVALID;
     s.busy = true;
   }
+  uint64_t span = 0;  // bytes [0, span) of the slot hold every packet
+  for (uint64_t i = 0; i < count; ++i) {
+    const uint64_t o = s.h_offsets[i], l = s.h_lengths[i];
+    if (o > r->slot_bytes || l > r->slot_bytes - o) {
+      std::lock_guard<std::mutex> lk(r->lock);
+      s.busy = false;
+      return ENET_CRC_E_INVALID;
+    }
+    span = std::max(span, o + l);
+  }
   DeviceGuard g(r->device);
-  auto fail = [&](hipError_t e) {
-    std::lock_guard<std::mutex> lk(r->lock);
-    s.busy = false;
-    return fail_hip(e);
-  };
   hipError_t e = hipSuccess;
   if (count) {
     if (span) e = hipMemcpyAsync(s.d_data, s.h_data, span, hipMemcpyHostToDevice, s.stream);
@@ -526,7 +790,12 @@ int enet_crc_ring_submit(enet_crc_ring* r, uint32_t slot, uint64_t count) {
       e = hipMemcpyAsync(s.h_crcs, s.d_crcs, count * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream);
   }
   if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
-  if (e != hipSuccess) return fail(e);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s.stream);  // nothing queued may outlive the failed submit
+    std::lock_guard<std::mutex> lk(r->lock);
+    s.busy = false;
+    return fail_hip(e);
+  }
   return ENET_CRC_OK;
 }
 
@@ -547,7 +816,7 @@ int enet_crc_ring_wait(enet_crc_ring* r, uint32_t slot) {
 }  // extern "C"
 
 // ---------------------------------------------------------------------------------
-// Batched range coder (include/enet_range_amd.h; kernels in range_coder.hip).
+// Range coder (include/enet_range_amd.h; kernels in range_coder.hip).
 
 static int range_batch(bool decompress, const void* d_in, const uint64_t* d_in_offsets,
                        const uint32_t* d_in_lengths, uint64_t count, void* d_out, const uint64_t* d_out_offsets,
@@ -559,11 +828,82 @@ static int range_batch(bool decompress, const void* d_in, const uint64_t* d_in_o
     return ENET_CRC_E_INVALID;
   const uint64_t workers = scratch_bytes / kRangeArenaBytes;
   if (workers == 0) return ENET_CRC_E_INVALID;
+  const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  DeviceGuard g(stream_device(stream));
   hipError_t e = launch_range(decompress, static_cast<const uint8_t*>(d_in), d_in_offsets, d_in_lengths, count,
                               static_cast<uint8_t*>(d_out), d_out_offsets, d_out_limits, d_sizes, d_scratch, workers,
-                              static_cast<hipStream_t>(hip_stream));
+                              stream);
   return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
 }
+
+namespace {
+
+// Host-memory range-coder batch on lane 0 of `ctx` (caller holds the context lock).
+// Packet p's input is in_len[p] bytes at h_in + in_off[p] (h_in == NULL: the bytes are
+// already in R.in.h at in_off[p]); its output goes to h_out + out_off[p], at most
+// out_lim[p] bytes; sizes[p] = the coder's return value.  Only the first sizes[p]
+// bytes of each output window are written.
+int range_host(enet_crc_ctx* ctx, bool decompress, const uint8_t* h_in, const uint64_t* in_off,
+               const uint32_t* in_len, uint64_t count, uint8_t* h_out, const uint64_t* out_off,
+               const uint32_t* out_lim, uint32_t* sizes) {
+  if (count == 0) return ENET_CRC_OK;
+  Lane& L = ctx->lanes[0];
+  RangeStage& R = L.range;
+  DeviceGuard g(L.device);
+  quiesce(L);
+  const hipStream_t st = L.slot[0].stream;
+  uint64_t ilo = UINT64_MAX, ihi = 0, olo = UINT64_MAX, ohi = 0;
+  for (uint64_t p = 0; p < count; ++p) {
+    ilo = std::min(ilo, in_off[p]);
+    ihi = std::max(ihi, in_off[p] + in_len[p]);
+    olo = std::min(olo, out_off[p]);
+    ohi = std::max(ohi, out_off[p] + out_lim[p]);
+  }
+  if (h_in == nullptr) ilo = 0;  // staged at its own offsets
+  const size_t ispan = (size_t)(ihi - ilo), ospan = (size_t)(ohi - olo);
+  if (h_in) ENET_TRY(R.in.grow(std::max<size_t>(ispan, 1), 16));
+  ENET_TRY(R.out.grow(std::max<size_t>(ospan, 1), 16));
+  ENET_TRY(R.in_off.grow(count));
+  ENET_TRY(R.out_off.grow(count));
+  ENET_TRY(R.in_len.grow(count));
+  ENET_TRY(R.out_lim.grow(count));
+  ENET_TRY(R.sizes.grow(count));
+  const uint64_t workers = std::min<uint64_t>(count, kRangeHostWorkers);
+  if (workers > R.workers) {
+    if (R.d_scratch) (void)hipFree(R.d_scratch);
+    R.d_scratch = nullptr;
+    R.workers = 0;
+    ENET_HIP_TRY(hipMalloc(&R.d_scratch, workers * kRangeArenaBytes));
+    R.workers = workers;
+  }
+  if (h_in) memcpy(R.in.h, h_in + ilo, ispan);
+  for (uint64_t p = 0; p < count; ++p) {
+    R.in_off.h[p] = in_off[p] - ilo;
+    R.in_len.h[p] = in_len[p];
+    R.out_off.h[p] = out_off[p] - olo;
+    R.out_lim.h[p] = out_lim[p];
+  }
+  L.slot[0].busy = true;  // quiesce() waits for this stream on an error exit
+  ENET_HIP_TRY(hipMemcpyAsync(R.in.d, R.in.h, std::max<size_t>(ispan, 1), hipMemcpyHostToDevice, st));
+  ENET_HIP_TRY(hipMemcpyAsync(R.in_off.d, R.in_off.h, count * 8, hipMemcpyHostToDevice, st));
+  ENET_HIP_TRY(hipMemcpyAsync(R.in_len.d, R.in_len.h, count * 4, hipMemcpyHostToDevice, st));
+  ENET_HIP_TRY(hipMemcpyAsync(R.out_off.d, R.out_off.h, count * 8, hipMemcpyHostToDevice, st));
+  ENET_HIP_TRY(hipMemcpyAsync(R.out_lim.d, R.out_lim.h, count * 4, hipMemcpyHostToDevice, st));
+  ENET_HIP_TRY(launch_range(decompress, R.in.d, R.in_off.d, R.in_len.d, count, R.out.d, R.out_off.d, R.out_lim.d,
+                            R.sizes.d, R.d_scratch, R.workers, st));
+  ENET_HIP_TRY(hipMemcpyAsync(R.sizes.h, R.sizes.d, count * 4, hipMemcpyDeviceToHost, st));
+  if (ospan) ENET_HIP_TRY(hipMemcpyAsync(R.out.h, R.out.d, ospan, hipMemcpyDeviceToHost, st));
+  ENET_HIP_TRY(hipStreamSynchronize(st));
+  L.slot[0].busy = false;
+  for (uint64_t p = 0; p < count; ++p) {
+    const uint32_t n = std::min(R.sizes.h[p], out_lim[p]);
+    sizes[p] = R.sizes.h[p];
+    if (n) memcpy(h_out + out_off[p], R.out.h + R.out_off.h[p], n);
+  }
+  return ENET_CRC_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -584,6 +924,88 @@ int enet_range_decompress_ragged_device(const void* d_in, const uint64_t* d_in_o
                                         void* hip_stream) {
   return range_batch(true, d_in, d_in_offsets, d_in_lengths, count, d_out, d_out_offsets, d_out_limits, d_sizes,
                      d_scratch, scratch_bytes, hip_stream);
+}
+
+int enet_range_compress_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, size_t in_limit,
+                            uint8_t* out, size_t out_limit, size_t* out_size) {
+  if (!ctx || !out_size || (nbufs > 0 && !bufs) || (out_limit > 0 && !out)) return ENET_CRC_E_INVALID;
+  *out_size = 0;
+  if (out_limit > 0xFFFFFFFFull) out_limit = 0xFFFFFFFFull;  // the window is u32-sized
+  // compress.rs:79: no slices or a zero in_limit codes nothing.
+  if (nbufs == 0 || in_limit == 0) return ENET_CRC_OK;
+  // The byte sequence compress.rs:103-126 reads: the slices in order, except that an
+  // empty slice after the first reads as one 0 byte (NonNull::dangling(), c.rs:79-85).
+  size_t total = 0;
+  for (size_t i = 0; i < nbufs; ++i) {
+    if (bufs[i].len > 0 && !bufs[i].data) return ENET_CRC_E_INVALID;
+    total += bufs[i].len ? bufs[i].len : (i > 0 ? 1 : 0);
+  }
+  if (total > 0xFFFFFFFFull) return ENET_CRC_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  RangeStage& R = ctx->lanes[0].range;
+  {
+    DeviceGuard g(ctx->lanes[0].device);
+    quiesce(ctx->lanes[0]);
+    ENET_TRY(R.in.grow(std::max<size_t>(total, 1), 16));
+  }
+  size_t pos = 0;
+  for (size_t i = 0; i < nbufs; ++i) {
+    if (bufs[i].len) {
+      memcpy(R.in.h + pos, bufs[i].data, bufs[i].len);
+      pos += bufs[i].len;
+    } else if (i > 0) {
+      R.in.h[pos++] = 0;
+    }
+  }
+  const uint64_t off0 = 0;
+  const uint32_t len = (uint32_t)total, lim = (uint32_t)out_limit;
+  uint32_t size = 0;
+  ENET_TRY(range_host(ctx, false, nullptr, &off0, &len, 1, out, &off0, &lim, &size));
+  *out_size = size;
+  return ENET_CRC_OK;
+}
+
+int enet_range_decompress(enet_crc_ctx* ctx, const uint8_t* in, size_t in_len, uint8_t* out, size_t out_limit,
+                          size_t* out_size) {
+  if (!ctx || !out_size || (in_len > 0 && !in) || (out_limit > 0 && !out)) return ENET_CRC_E_INVALID;
+  *out_size = 0;
+  if (in_len > 0xFFFFFFFFull) return ENET_CRC_E_INVALID;
+  if (out_limit > 0xFFFFFFFFull) out_limit = 0xFFFFFFFFull;
+  if (in_len == 0) return ENET_CRC_OK;  // compress.rs:481-483
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  const uint64_t off0 = 0;
+  const uint32_t len = (uint32_t)in_len, lim = (uint32_t)out_limit;
+  uint32_t size = 0;
+  ENET_TRY(range_host(ctx, true, in, &off0, &len, 1, out, &off0, &lim, &size));
+  *out_size = size;
+  return ENET_CRC_OK;
+}
+
+static int range_ragged_host(enet_crc_ctx* ctx, bool decompress, const void* h_in, const uint64_t* h_in_offsets,
+                             const uint32_t* h_in_lengths, uint64_t count, void* h_out,
+                             const uint64_t* h_out_offsets, const uint32_t* h_out_limits, uint32_t* h_sizes) {
+  if (!ctx) return ENET_CRC_E_INVALID;
+  if (count == 0) return ENET_CRC_OK;
+  if (!h_in || !h_in_offsets || !h_in_lengths || !h_out || !h_out_offsets || !h_out_limits || !h_sizes)
+    return ENET_CRC_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  return range_host(ctx, decompress, static_cast<const uint8_t*>(h_in), h_in_offsets, h_in_lengths, count,
+                    static_cast<uint8_t*>(h_out), h_out_offsets, h_out_limits, h_sizes);
+}
+
+int enet_range_compress_ragged_host(enet_crc_ctx* ctx, const void* h_in, const uint64_t* h_in_offsets,
+                                    const uint32_t* h_in_lengths, uint64_t count, void* h_out,
+                                    const uint64_t* h_out_offsets, const uint32_t* h_out_limits, uint32_t* h_sizes) {
+  return range_ragged_host(ctx, false, h_in, h_in_offsets, h_in_lengths, count, h_out, h_out_offsets, h_out_limits,
+                           h_sizes);
+}
+
+int enet_range_decompress_ragged_host(enet_crc_ctx* ctx, const void* h_in, const uint64_t* h_in_offsets,
+                                      const uint32_t* h_in_lengths, uint64_t count, void* h_out,
+                                      const uint64_t* h_out_offsets, const uint32_t* h_out_limits,
+                                      uint32_t* h_sizes) {
+  return range_ragged_host(ctx, true, h_in, h_in_offsets, h_in_lengths, count, h_out, h_out_offsets, h_out_limits,
+                           h_sizes);
 }
 
 }  // extern "C"

@@ -33,6 +33,7 @@ HEADER_FLAG_MASK = 0xC000
 HEADER_FLAG_SENT_TIME = 0x8000
 HEADER_FLAG_COMPRESSED = 0x4000
 PROTOCOL_MAXIMUM_PEER_ID = 4095
+PROTOCOL_MAXIMUM_MTU = 4096  # src/consts.rs:8; the receive buffers are [u8; 4096] (c/host.rs:37)
 
 
 def parse_header(datagram, checksum: bool = True):
@@ -49,7 +50,8 @@ def parse_header(datagram, checksum: bool = True):
     return peer_id, flags, header_size
 
 
-def verify_received(datagrams: Sequence, connect_id_of: Callable[[int], int], ctx=None) -> list:
+def verify_received(datagrams: Sequence, connect_id_of: Callable[[int], int], ctx=None,
+                    compressor: Optional[bool] = None) -> list:
     """Receive-side checksum verdicts for a batch of datagrams, in arrival order.
 
     ``connect_id_of(peer_id)`` is called per datagram, in order, at the moment the
@@ -57,25 +59,56 @@ def verify_received(datagrams: Sequence, connect_id_of: Callable[[int], int], ct
     for peer id 4095 (slot value 0).  Returns one bool per datagram (True = accept);
     datagrams too short for their header are rejected, as the reference returns
     before reaching the checksum (:1396-1398, :1412-1415 with :1440-1450).
+
+    Compressed datagrams (HEADER_FLAG_COMPRESSED, :1441-1469): with ``compressor``
+    true (the host has the range coder installed) the payload after the header is
+    decompressed first, on the GPU, into a window of 4096 - header_size bytes, and the
+    checksum covers the header plus the decompressed bytes, as in the reference; a
+    size of 0 or one past the window drops the datagram (:1456-1460).  Without a
+    compressor a compressed datagram is dropped (:1442-1444).
     """
     ctx = ctx or default_context(0)
     n = len(datagrams)
     if n == 0:
         return []
-    lens = np.array([len(d) for d in datagrams], dtype=np.uint32)
+    views = [bytes(d) for d in datagrams]
+    hdrs = [parse_header(d) for d in views]
+    # Decompress the flagged payloads in one batch (only those that reach :1442).
+    comp = [i for i, (d, h) in enumerate(zip(views, hdrs))
+            if h is not None and h[1] & HEADER_FLAG_COMPRESSED and compressor and h[2] <= len(d)]
+    if comp:
+        payloads = [views[i][hdrs[i][2]:] for i in comp]
+        p_len = np.array([len(p) for p in payloads], dtype=np.uint32)
+        p_off = np.zeros(len(comp), dtype=np.uint64)
+        if len(comp) > 1:
+            p_off[1:] = np.cumsum(p_len[:-1], dtype=np.uint64)
+        limits = np.array([PROTOCOL_MAXIMUM_MTU - hdrs[i][2] for i in comp], dtype=np.uint32)
+        blob = np.frombuffer(b"".join(payloads) or b"\0", dtype=np.uint8)
+        out, o_off, sizes = ctx.range_ragged_host(True, blob, p_off, p_len, limits)
+        for k, i in enumerate(comp):
+            size = int(sizes[k])
+            if size == 0 or size > int(limits[k]):
+                views[i] = None
+            else:
+                start = int(o_off[k])
+                views[i] = views[i][:hdrs[i][2]] + out[start:start + size].tobytes()
+    lens = np.array([len(d) if d is not None else 0 for d in views], dtype=np.uint32)
     offs = np.zeros(n, dtype=np.uint64)
     if n > 1:
         offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
-    buf = np.frombuffer(b"".join(bytes(d) for d in datagrams), dtype=np.uint8) if lens.sum() else np.zeros(1, np.uint8)
+    joined = b"".join(d for d in views if d is not None)
+    buf = np.frombuffer(joined, dtype=np.uint8) if joined else np.zeros(1, np.uint8)
     crcs = ctx.crc32_ragged_host(buf, offs, lens)  # one GPU pass, slots as received
     out = []
-    for i, d in enumerate(datagrams):
-        hdr = parse_header(d)
-        if hdr is None or hdr[2] > len(d):
+    for i, (d, hdr) in enumerate(zip(views, hdrs)):
+        if hdr is None or d is None or hdr[2] > len(d):
             out.append(False)
             continue
-        peer_id, _, h = hdr
-        desired = int.from_bytes(bytes(d[h - 4:h]), "little")  # native-endian u32 (x86)
+        peer_id, flags, h = hdr
+        if flags & HEADER_FLAG_COMPRESSED and not compressor:
+            out.append(False)
+            continue
+        desired = int.from_bytes(d[h - 4:h], "little")  # native-endian u32 (x86)
         v = 0 if peer_id == PROTOCOL_MAXIMUM_PEER_ID else (connect_id_of(peer_id) & 0xFFFFFFFF)
         out.append(slot_adjust(int(crcs[i]), desired, v, len(d) - h) == desired)
     return out

@@ -7,10 +7,11 @@ Reference interface (jabuwu/rusty_enet v0.4.0, src/compressor.rs):
   * ``RangeCoder::new()`` (:22-28) and its impl (:36-69) over src/c/compress.rs.
 
 ``RangeCoder.compress`` / ``.decompress`` take the same arguments and return the same
-sizes (0 = not compressible within ``len(out)`` / malformed stream).  They run one
-packet through the batched device entry points, so they pay a launch and two PCIe
-copies per call; ``compress_batch`` / ``decompress_batch`` are the real interface
-(one launch for a whole batch of datagrams, include/enet_range_amd.h).  There is no
+sizes (0 = not compressible within ``len(out)`` / malformed stream); they call the
+host-memory C entry points ``enet_range_compress_iov`` / ``enet_range_decompress`` on a
+context that owns the arenas, so they pay a launch and two PCIe copies per call.
+``compress_batch`` / ``decompress_batch`` are the real interface (one launch for a
+whole batch of device-resident datagrams, include/enet_range_amd.h).  There is no
 CPU fallback: without the library or a device these raise.
 """
 from __future__ import annotations
@@ -42,18 +43,24 @@ def gather_slices(in_buffers: Sequence) -> bytes:
 _scratch = {}
 
 
-def _scratch_for(dev, workers: int):
-    """Arena scratch for `workers` coders: one pool per device, grown on demand and
-    shared by the launches of this process (they run in stream order on the caller's
-    stream; concurrent launches on different streams need their own scratch)."""
+def _scratch_for(dev, stream, workers: int):
+    """Arena scratch for `workers` coders, one buffer per (device, stream), grown on
+    demand.  Launches on one stream run in order, so they can share a buffer; launches
+    on different streams get different buffers (no race on the arenas).  A buffer that
+    is replaced is marked as used by its stream first, so torch's caching allocator does
+    not hand it out again while a launch on that stream may still be reading it."""
     import torch
 
     need = int(lib().enet_range_scratch_bytes(workers))
-    buf = _scratch.get(str(dev))
+    key = (str(dev), int(stream.cuda_stream))
+    buf = _scratch.get(key)
     if buf is None or buf.numel() < need:
-        _scratch.pop(str(dev), None)
-        buf = torch.empty(need, dtype=torch.uint8, device=dev)
-        _scratch[str(dev)] = buf
+        old = _scratch.pop(key, None)
+        if old is not None:
+            old.record_stream(stream)
+        with torch.cuda.stream(stream):
+            buf = torch.empty(need, dtype=torch.uint8, device=dev)
+        _scratch[key] = buf
     return buf[:need]
 
 
@@ -62,23 +69,29 @@ def _run(decompress: bool, data, in_offsets, in_lengths, out_offsets, out_limits
     import torch
 
     dev = data.device
+    if not data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
+        raise ValueError("data must be a contiguous uint8 device tensor")
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    elif stream.device != dev:
+        raise ValueError("stream must belong to the data's device")
     n = int(in_lengths.numel())
-    out = torch.empty(max(out_bytes, 1), dtype=torch.uint8, device=dev)
-    sizes = torch.empty(n, dtype=torch.int32, device=dev)
+    with torch.cuda.stream(stream):
+        out = torch.empty(max(out_bytes, 1), dtype=torch.uint8, device=dev)
+        sizes = torch.empty(n, dtype=torch.int32, device=dev)
     if n == 0:
         return out, sizes
     w = min(n, workers or DEFAULT_WORKERS)
-    scratch = _scratch_for(dev, w)
+    scratch = _scratch_for(dev, stream, w)
     for t, dt in ((in_offsets, torch.int64), (in_lengths, torch.int32), (out_offsets, torch.int64),
                   (out_limits, torch.int32)):
-        if t.device != dev or t.dtype != dt or not t.is_contiguous():
-            raise ValueError("offsets must be contiguous int64 and lengths/limits int32 on the data's device")
-    if stream is None:
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        if t.device != dev or t.dtype != dt or not t.is_contiguous() or t.numel() != n:
+            raise ValueError("offsets must be contiguous int64 and lengths/limits int32 on the data's device, "
+                             "one entry per packet")
     fn = lib().enet_range_decompress_ragged_device if decompress else lib().enet_range_compress_ragged_device
     check(fn(data.data_ptr(), in_offsets.data_ptr(), in_lengths.data_ptr(), n, out.data_ptr(),
              out_offsets.data_ptr(), out_limits.data_ptr(), sizes.data_ptr(), scratch.data_ptr(),
-             scratch.numel(), stream),
+             scratch.numel(), stream.cuda_stream),
           "enet_range_decompress_ragged_device" if decompress else "enet_range_compress_ragged_device")
     return out, sizes
 
@@ -120,38 +133,18 @@ def decompress_batch(data, in_offsets, in_lengths, out_limits, workers: Optional
 class RangeCoder:
     """``RangeCoder`` (src/compressor.rs:17-69) on the GPU.  ``compress`` and
     ``decompress`` follow the `Compressor` trait: they write into ``out`` (a writable
-    buffer: bytearray, numpy array, memoryview) and return the byte count."""
+    buffer: bytearray, numpy array, memoryview) and return the byte count.  Backed by
+    a context's host-memory entry points (the context owns the arena scratch)."""
 
-    def __init__(self, device: int = 0):
-        import torch
+    def __init__(self, device: int = 0, ctx=None):
+        from .checksum import Context
 
-        self.dev = torch.device("cuda", device)
-
-    def _one(self, decompress: bool, payload: bytes, out) -> int:
-        import torch
-
-        view = memoryview(out).cast("B")
-        limit = len(view)
-        src = torch.from_numpy(np.frombuffer(payload or b"\x00", dtype=np.uint8).copy()).to(self.dev)
-        offs = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        lens = torch.tensor([len(payload)], dtype=torch.int32, device=self.dev)
-        lims = torch.tensor([limit], dtype=torch.int32, device=self.dev)
-        res, sizes = _run(decompress, src, offs, lens, offs, lims, limit, 1, None)
-        n = int(sizes.cpu()[0])
-        if n:
-            view[:n] = res[:n].cpu().numpy().tobytes()
-        return n
+        self.ctx = ctx if ctx is not None else Context(device)
 
     def compress(self, in_buffers: Sequence, in_limit: int, out) -> int:
-        """compressor.rs:38-57 / compress.rs:60-462.  ``in_limit`` only gates an empty
-        call (compress.rs:79), as in the reference."""
-        if len(in_buffers) == 0 or in_limit <= 0:
-            return 0
-        return self._one(False, gather_slices(in_buffers), out)
+        """compressor.rs:38-57 / compress.rs:60-462."""
+        return self.ctx.range_compress(in_buffers, in_limit, out)
 
     def decompress(self, in_data, out) -> int:
         """compressor.rs:59-68 / compress.rs:463-987."""
-        payload = bytes(in_data)
-        if len(payload) == 0:
-            return 0
-        return self._one(True, payload, out)
+        return self.ctx.range_decompress(in_data, out)

@@ -2,6 +2,9 @@
 
     python scripts/traffic_summary.py gpurun_out/<tag> [--write profiles/pmc_traffic.json]
 
+Each entry records the hash of the kernel sources it was measured on (bench.py
+kernel_source_hash); bench.py reports the traffic only while that hash still matches.
+
 FETCH_SIZE is reported in KiB and, on gfx950, counts half the bytes of 16-B-per-lane
 streaming reads (MI355X_MICROARCH.md, HBM section): bytes = FETCH_SIZE * 1024 * 2.
 """
@@ -12,7 +15,11 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_source_hash  # noqa: E402
+
 root = sys.argv[1]
+src_hash = kernel_source_hash()
 out = {}
 for cfg in ("uniform", "ragged", "large"):
     fetch, dur = {}, {}
@@ -34,7 +41,7 @@ for cfg in ("uniform", "ragged", "large"):
                       "mean_duration_ns": dur.get(k)}
     main = max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
     out[cfg] = {"kernel": main, "hbm_bytes_per_launch": kernels[main]["hbm_bytes_per_launch"],
-                "kernels": kernels, "source": os.path.relpath(root)}
+                "kernels": kernels, "source": os.path.relpath(root), "source_hash": src_hash}
 print(json.dumps(out, indent=1))
 if "--write" in sys.argv:
     with open(sys.argv[sys.argv.index("--write") + 1], "w") as f:

@@ -26,6 +26,10 @@ def test_header_declares_expected_api():
     assert {"enet_crc_ring_create", "enet_crc_ring_submit", "enet_crc_ring_wait"} <= set(syms)
     assert {"enet_range_compress_ragged_device", "enet_range_decompress_ragged_device",
             "enet_range_scratch_bytes"} <= set(syms)
+    assert {"enet_crc_ctx_create_multi", "enet_crc_ctx_lanes", "enet_crc_shard_bounds", "enet_crc32_shards_device",
+            "enet_crc_ctx_set_percall_mode"} <= set(syms)
+    assert {"enet_range_compress_iov", "enet_range_decompress", "enet_range_compress_ragged_host",
+            "enet_range_decompress_ragged_host"} <= set(syms)
     assert sorted(_native.exported_symbols()) == syms
 
 
@@ -33,7 +37,7 @@ def test_library_exports_every_declared_symbol():
     lib = _native.lib()
     for name in _declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.enet_crc_abi_version() == _native.ABI_VERSION == 2
+    assert lib.enet_crc_abi_version() == _native.ABI_VERSION == 3
     assert lib.enet_crc_strerror(0) == b"ok"
     assert lib.enet_crc_strerror(_native.ENET_CRC_E_NO_DEVICE) == b"no usable HIP device"
 
@@ -76,3 +80,40 @@ def test_no_device_fails_loudly():
     args[3] = 4
     assert lib.enet_range_compress_ragged_device(*args) == _native.ENET_CRC_E_INVALID
     assert lib.enet_range_decompress_ragged_device(*args) == _native.ENET_CRC_E_INVALID
+    # multi-device context: argument checks, then the device check
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert lib.enet_crc_ctx_create_multi(devs, 0, ctypes.byref(handle)) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_crc_ctx_create_multi(None, 2, ctypes.byref(handle)) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_crc_ctx_create_multi(devs, 2, ctypes.byref(handle)) == _native.ENET_CRC_E_NO_DEVICE
+    assert not handle.value
+    assert lib.enet_crc_ctx_lanes(None) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_crc_ctx_set_percall_mode(None, 1) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_crc32_shards_device(None, 0) == 0
+    assert lib.enet_crc32_shards_device(None, 1) == _native.ENET_CRC_E_INVALID
+    size = ctypes.c_size_t()
+    assert lib.enet_range_compress_iov(None, None, 0, 1, None, 0, ctypes.byref(size)) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_range_decompress(None, None, 0, None, 0, ctypes.byref(size)) == _native.ENET_CRC_E_INVALID
+    assert lib.enet_range_compress_ragged_host(None, *([None] * 3), 0, *([None] * 4)) == _native.ENET_CRC_E_INVALID
+
+
+def test_native_shard_bounds_match_python_split():
+    """enet_crc_shard_bounds (C++) == rusty_enet_amd.shards.shard_bounds (no device work)."""
+    import numpy as np
+
+    from _data import ENET_SEED, ragged_lengths
+    from rusty_enet_amd.checksum import shard_bounds_native
+    from rusty_enet_amd.shards import shard_bounds
+
+    cases = [ragged_lengths(ENET_SEED, 100_000), ragged_lengths(7, 13, lo=0, hi=5000),
+             np.array([], dtype=np.uint32), np.array([1000], dtype=np.uint32), np.zeros(10, dtype=np.uint32),
+             np.array([0, 0, 7, 0, 0, 0, 9], dtype=np.uint32), np.full(17, 0xFFFFFFFF, dtype=np.uint32)]
+    for ln in cases:
+        for world in (1, 2, 3, 4, 7, 8, 64):
+            got = shard_bounds_native(lengths=ln, nshards=world)
+            want = [shard_bounds(world, r, lengths=ln) for r in range(world)]
+            assert [(int(got[r]), int(got[r + 1])) for r in range(world)] == want, (ln.size, world)
+    for count in (0, 1, 7, 1 << 20, (1 << 20) + 5):
+        for world in (1, 2, 3, 8):
+            got = shard_bounds_native(count=count, nshards=world)
+            assert [(int(got[r]), int(got[r + 1])) for r in range(world)] == \
+                [shard_bounds(world, r, count=count) for r in range(world)]

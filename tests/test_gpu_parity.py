@@ -152,6 +152,30 @@ def test_full_size_ragged_1m(dev):
     assert np.array_equal(got, _oracle.crc32_ragged(d.cpu().numpy(), offsets, lengths))
 
 
+def test_full_shard_uniform_2m_x_1200(dev):
+    """The per-GPU shard of configs[3] (16M x 1200 B over 8 GPUs): 2M x 1200 B = 2.4 GB."""
+    n, L = 2 << 20, 1200
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED + 3)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    got = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
+    want = _oracle.crc32_uniform(d.cpu().numpy(), L, L, n, threads=16)
+    del d
+    assert np.array_equal(got, want)
+
+
+def test_full_shard_large_32768_x_64k(dev):
+    """The per-GPU shard of configs[4] (256K x 64 KiB over 8 GPUs): 32768 x 64 KiB = 2 GiB."""
+    n, L = 32768, 65536
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED + 4)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    got = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
+    want = _oracle.crc32_uniform(d.cpu().numpy(), L, L, n, threads=16)
+    del d
+    assert np.array_equal(got, want)
+
+
 # --- properties --------------------------------------------------------------------
 
 def test_single_bit_flips_are_detected(dev):
