@@ -328,18 +328,34 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
     pkt = [data[:1392]]
     if ctx.crc32(pkt) != _oracle.crc32(pkt):
         raise SystemExit("bench: per-call checksum differs from the oracle")
-    for _ in range(50):
-        ctx.crc32(pkt)
+    from rusty_enet_amd import _native
+
+    variants = {}
+    for name, mode in (("copy", _native.ENET_CRC_PERCALL_COPY), ("zerocopy", _native.ENET_CRC_PERCALL_ZEROCOPY)):
+        ctx.set_percall_mode(mode)
+        if ctx.crc32(pkt) != _oracle.crc32(pkt):
+            raise SystemExit(f"bench: per-call ({name}) checksum differs from the oracle")
+        for _ in range(50):
+            ctx.crc32(pkt)
+        calls = 2000
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            ctx.crc32(pkt)
+        variants[name] = round((time.perf_counter() - t0) / calls * 1e6, 2)
+    per_call_us = variants["zerocopy"]  # the context's default mode
+    # The reference's own per-call cost for the same datagram: the oracle's Sarwate loop on one core.
     t0 = time.perf_counter()
-    calls = 2000
-    for _ in range(calls):
-        ctx.crc32(pkt)
-    per_call_us = (time.perf_counter() - t0) / calls * 1e6
+    for _ in range(2000):
+        _oracle.crc32(pkt)
+    cpu_call_us = (time.perf_counter() - t0) / 2000 * 1e6
     ctx.close()
     return {"value": round(rate, 3), "unit": "GiB/s", "path": "enet_crc32_ragged_host",
             "sample": f"{n} x {L} B from pageable host memory, median of 5 passes",
             "per_call_us": round(per_call_us, 2),
-            "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000",
+            "per_call_variants_us": variants,
+            "per_call_cpu_oracle_us": round(cpu_call_us, 2),
+            "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000; "
+                               "cpu: the C restatement of src/crc32.rs on the same datagram through ctypes",
             "ring": ring_rate(dev, L)}
 
 

@@ -1198,6 +1198,294 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
   __builtin_amdgcn_s_waitcnt(0);
 }
 
+
+// ---------------------------------------------------------------------------------
+// Group-stream kernel: ragged batches in their own order, no pre-pass.
+//
+// The 8 groups of a wave are independent consumers of one in-order packet queue:
+// when a group finishes a packet it takes the next unassigned one (ballot rank, no
+// atomics), so a group never waits for the others and no slot is padded to a round's
+// longest packet.  Consecutive packets are in flight in neighbouring groups at the
+// same time, so the 128-B line two packets share is read twice within a few steps
+// (from L2), not twice from HBM as after a sort by length.
+//
+// Pipeline per wave (kGsRing slots of 1 KiB in a register ring; the slot loop is
+// unrolled by the ring depth so every ring register is statically indexed):
+//   producer, kGsRing steps ahead: assign packets to groups without one, issue each
+//     lane's 16-B load (global_load_dwordx4, unconditional: chunks outside a packet
+//     read the zero chunk) and the step's metadata (top-word masking, last step, id);
+//   consumer: mask, one Horner step on the 4 word streams (same arithmetic and tables
+//     as every other kernel here), and at a packet's last step PARK the group's 4x8
+//     stream values in LDS at the next column of a wave-wide park row, then zero them.
+//     When a row holds 8 packets, one combine pass turns it into 8 checksums with every
+//     lane busy (combine_streams: in-lane Horner + DPP tree inside 8-lane groups).
+// Work distribution: tasks of kGsTask consecutive packets; workgroup b owns tasks
+// b*16 + j + i*16*grid and its waves claim them in order from an LDS counter; the
+// groups of a wave flow from one claimed task into the next without synchronising.
+// Descriptors: once per ring cycle every lane reloads two (offset, length) pairs of the
+// next kGsAhead tasks into the wave's LDS ring of task buffers (rewrites of unchanged
+// entries are harmless).  The queue advances at most 8 packets per step, i.e. at most
+// 3 tasks per cycle, so the tasks it reaches in a cycle were written by the previous
+// cycle's reload: no wait, and every load stays unconditional (hipcc's vmcnt exact).
+// ---------------------------------------------------------------------------------
+constexpr int kGsRing = 5;                               // slots in flight per wave
+constexpr int kGsTask = 16;                              // packets per task
+constexpr int kGsAhead = 2 * 64 / kGsTask;               // tasks one reload covers (2 per lane)
+constexpr int kGsBufs = kGsAhead + 1;                    // task buffers (the current one + kGsAhead)
+static_assert((kGsTask - 1 + 8 * kGsRing) / kGsTask + 3 <= kGsAhead, "a cycle reaches only reloaded tasks");
+constexpr uint32_t kGsHead = 1u << 0;                    // lane's chunk holds the packet's top word
+constexpr uint32_t kGsJ0Shift = 1;                       // 2 bits: index of the top word in the chunk
+constexpr uint32_t kGsVShift = 3;                        // 2 bits: sa - top
+constexpr uint32_t kGsLast = 1u << 5;                    // last step of the group's packet
+constexpr uint32_t kGsZShift = 6;                        // 2 bits: bytes run past the packet end (lane 0)
+constexpr uint32_t kGsFallback = 1u << 8;                // chunk begins before the caller's buffer
+constexpr uint32_t kGsFbShift = 9;                       // 2 bits: (chunk - (base4 - 16)) / 4
+constexpr uint32_t kGsIdle = 0xFFFFFFFFu;                // group has no packet and will get none
+
+struct GsLds {
+  uint32_t tables[kLdsDwords];
+  uint64_t doff[kWavesPerBlock][kGsBufs][kGsTask];
+  uint32_t dlen[kWavesPerBlock][kGsBufs][kGsTask];
+  u32x4 park[kWavesPerBlock][2][64];
+  uint32_t pmeta[kWavesPerBlock][2][8][2];  // packet id, z
+  uint64_t claim[kWavesPerBlock][kGsBufs];  // task of sequence number s at [s % kGsBufs]
+  uint32_t next_dispatch;
+};
+static_assert(sizeof(GsLds) <= 160 * 1024, "LDS");
+
+struct GsBatch {
+  uint64_t base;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
+  uint64_t count;
+};
+
+typedef __attribute__((address_space(1))) const uint64_t GlobalU64;
+typedef __attribute__((address_space(1))) uint32_t GlobalOutU32;
+
+__global__ __launch_bounds__(kBlock) void crc32_group_stream_kernel(GsBatch batch, uint32_t* out_ptr) {
+  __shared__ __attribute__((aligned(16))) GsLds S;
+  // The batch in locals (lambdas capture these, not the by-value kernel argument) and
+  // global-address-space pointers (global_load/store, never flat: flat ops count on
+  // lgkmcnt too and would order against the LDS lookups).
+  const uint64_t base = batch.base, count = batch.count;
+  GlobalU64* const offsets = (GlobalU64*)batch.offsets;
+  GlobalU32* const lengths = (GlobalU32*)batch.lengths;
+  GlobalOutU32* const out = (GlobalOutU32*)out_ptr;
+  uint32_t* const lds = S.tables;
+  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kGsBufs;
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(base);
+  const uint32_t lane = threadIdx.x & 63u, k = c.k, lead = lane & ~7u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t ntasks = (count + kGsTask - 1) / kGsTask;
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto task_of = [&](uint32_t d) __attribute__((always_inline)) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
+  // Claimed tasks: S.claim holds the tasks of sequence numbers seq .. seq + kGsAhead;
+  // tk0 / tk1 (wave-uniform) are those of seq and seq + 1.
+  const uint64_t tk_first = task_of(wv);
+  if (tk_first >= ntasks) return;
+  if (lane < (uint32_t)kGsBufs) S.claim[wv][lane] = task_of(wv + kWavesPerBlock * lane);
+  uint64_t tk0 = tk_first, tk1 = task_of(wv + kWavesPerBlock);
+  uint32_t seq = 0;  // sequence number of tk0 (the task the queue is in)
+  uint32_t idx = 0;  // queue position inside tk0
+
+  auto desc_src = [&](uint64_t t, uint32_t i) __attribute__((always_inline)) -> uint64_t {
+    const uint64_t p = t * kGsTask + i;
+    return p < count ? p : count - 1;
+  };
+  // Reload: lane l, pair r -> packet l % kGsTask of the task seq + 1 + l / kGsTask + 4r.
+  uint64_t ld_off0 = 0, ld_off1 = 0;
+  uint32_t ld_len0 = 0, ld_len1 = 0, ld_seq = 0;
+  const uint32_t di = lane % kGsTask, da = lane / kGsTask;
+  auto desc_issue = [&]() __attribute__((always_inline)) {
+    const uint64_t t0 = S.claim[wv][(seq + 1 + da) % kGsBufs];
+    const uint64_t t1 = S.claim[wv][(seq + 5 + da) % kGsBufs];
+    const uint64_t p0 = desc_src(t0, di), p1 = desc_src(t1, di);
+    ld_off0 = offsets[p0];
+    ld_len0 = lengths[p0];
+    ld_off1 = offsets[p1];
+    ld_len1 = lengths[p1];
+    ld_seq = seq;
+  };
+  auto desc_commit = [&]() __attribute__((always_inline)) {
+    const uint32_t s0 = ld_seq + 1 + da, s1 = ld_seq + 5 + da;
+    S.doff[wv][s0 % kGsBufs][di] = ld_off0;
+    S.dlen[wv][s0 % kGsBufs][di] = ld_len0;
+    S.doff[wv][s1 % kGsBufs][di] = ld_off1;
+    S.dlen[wv][s1 % kGsBufs][di] = ld_len1;
+  };
+  {  // the current task's descriptors, then the reload of the next kGsAhead
+    const uint64_t p0 = desc_src(tk0, di);
+    const uint64_t o0 = offsets[p0];
+    const uint32_t l0 = lengths[p0];
+    S.doff[wv][0][di] = o0;
+    S.dlen[wv][0][di] = l0;
+  }
+  desc_issue();
+  desc_commit();
+
+  // ---- producer state (group-uniform values in every lane of the group) ----
+  uint64_t pa = 0;         // this lane's chunk address at the group's next step
+  uint32_t rem = 0;        // steps left in the group's packet (0: needs one)
+  uint32_t pid = 0;        // packet id, or kGsIdle
+  uint32_t topf = 0;       // flags of the packet's first step
+  uint32_t zl = 0;         // z << kGsZShift of the packet (for its last step)
+  bool first = false;      // next step is the packet's first
+  bool top_dummy = false;  // this lane reads the zero chunk at the first step
+
+  // Give every group that needs a packet the next one in queue order (at most 8 per
+  // step).  An empty packet is answered on the spot; its group takes another next step.
+  auto assign = [&]() __attribute__((always_inline)) {
+    const uint64_t need = __builtin_amdgcn_ballot_w64(k == 0 && rem == 0 && pid != kGsIdle);
+    if (need == 0) return;
+    const bool mine = (need >> lead) & 1ull;
+    const uint32_t pos = idx + (uint32_t)__builtin_popcountll(need & ((1ull << lead) - 1ull));
+    if (mine) {
+      const uint32_t tsel = pos / kGsTask;  // 0: tk0, 1: tk1 (pos < 2 kGsTask)
+      const uint64_t t = tsel ? tk1 : tk0;
+      const uint32_t i = pos % kGsTask;
+      const uint64_t p = t * kGsTask + i;
+      if (t >= ntasks || p >= count) {
+        pid = kGsIdle;  // the queue is exhausted: nothing follows in this wave
+      } else {
+        const uint32_t buf = (seq + tsel) % kGsBufs;
+        const uint64_t sa = base + S.doff[wv][buf][i];
+        const uint32_t len = S.dlen[wv][buf][i];
+        pid = (uint32_t)p;
+        if (len == 0) {
+          if (k == 0) out[p] = 0u;  // crc32(&[]) == 0 (src/crc32.rs:40,46)
+        } else {
+          const uint64_t ea = sa + len;
+          const uint32_t z = (4u - (uint32_t)(ea & 3u)) & 3u;
+          const uint64_t ex = ea + z, top = sa & ~(uint64_t)3;
+          const uint64_t nwords = (ex - top) >> 2;
+          const uint32_t ns = (uint32_t)((((nwords + 3) >> 2) + kLanesPerPacket - 1) / kLanesPerPacket);
+          const uint64_t c0 = ex - 16u * (uint64_t)(k + 1u) - (uint64_t)kBytesPerStep * (ns - 1u);
+          const int64_t rel0 = (int64_t)(c0 - top);
+          const bool head = rel0 > -16 && rel0 <= 0;
+          const bool fb = head && c0 < c.base4;
+          uint32_t f = 0;
+          if (head) {
+            f = kGsHead | ((uint32_t)(-rel0 >> 2) << kGsJ0Shift) | ((uint32_t)(sa - top) << kGsVShift);
+            if (fb) f |= kGsFallback | ((uint32_t)((c0 + 16u - c.base4) >> 2) << kGsFbShift);
+          }
+          pa = c0;
+          rem = ns;
+          topf = f;
+          zl = z << kGsZShift;
+          first = true;
+          top_dummy = rel0 <= -16 || fb;
+        }
+      }
+    }
+    idx += (uint32_t)__builtin_popcountll(need);
+    if (idx >= (uint32_t)kGsTask) {  // into the next claimed task
+      idx -= kGsTask;
+      ++seq;
+      uint32_t d = 0;
+      if (lane == 0) {
+        d = atomicAdd(&S.next_dispatch, 1u);
+        S.claim[wv][(seq + kGsAhead) % kGsBufs] = task_of(d);
+      }
+      tk0 = tk1;
+      const uint64_t t1 = S.claim[wv][(seq + 1) % kGsBufs];
+      tk1 = __builtin_amdgcn_readfirstlane((uint32_t)t1) |
+            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t1 >> 32)) << 32);
+    }
+  };
+
+  // One producer step: the load and metadata of the group's next step into a ring slot.
+  auto produce = [&](u32x4& data, uint32_t& flags, uint32_t& id) __attribute__((always_inline)) {
+    assign();
+    const bool active = rem > 0;
+    uint64_t src = active && !(first && top_dummy) ? pa : c.dummy;
+    asm volatile("" : "+v"(src));  // ONE unconditional load (hipcc would otherwise branch between two)
+    uint32_t f = first ? topf : 0u;
+    if (active && rem == 1) f |= kGsLast | zl;
+    data = load_chunk(src);
+    flags = f;
+    id = pid;
+    pa += active ? (uint64_t)kBytesPerStep : 0u;  // branch-free: keeps the load out of any branch
+    rem -= active ? 1u : 0u;
+    first = false;
+    issue_order_fence();
+  };
+
+  // ---- consumer state ----
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+  uint32_t parked = 0;  // packets parked so far by this wave (row = (parked / 8) % 2)
+
+  auto combine_row = [&](uint32_t row, uint32_t ncols) __attribute__((always_inline)) {
+    const u32x4 hv = S.park[wv][row][lane];
+    const uint32_t col = lane >> 3;
+    const uint32_t id = S.pmeta[wv][row][col][0], z = S.pmeta[wv][row][col][1];
+    uint32_t reg = combine_streams(lds, hv.x, hv.y, hv.z, hv.w, c.lk);
+    if (z != 0 && k == 0) reg = unshift_zero_bytes(lds, reg, z);
+    if (k == 0 && col < ncols) out[id] = __builtin_bswap32(~reg);
+  };
+
+  auto consume = [&](const u32x4& data, uint32_t f, uint32_t id) __attribute__((always_inline)) {
+    uint32_t w0 = data.x, w1 = data.y, w2 = data.z, w3 = data.w;
+    const uint32_t j0 = (f >> kGsJ0Shift) & 3u;
+    if (__builtin_amdgcn_ballot_w64(f & kGsFallback)) {
+      if (f & kGsFallback) {
+        const uint64_t chunk = c.base4 - 16u + 4u * ((f >> kGsFbShift) & 3u);
+        load_top_words(chunk, 4u - j0, c.dummy, w0, w1, w2, w3);
+      }
+    }
+    const bool last = (f & kGsLast) != 0;
+    if (last && k == 0) w3 &= 0xFFFFFFFFu >> (8u * ((f >> kGsZShift) & 3u));  // data only, before injection
+    if (__builtin_amdgcn_ballot_w64(f & kGsHead)) {
+      if (f & kGsHead) mask_top((4u - j0) | (((f >> kGsVShift) & 3u) << kMetaVShift), w0, w1, w2, w3);
+    }
+    h0 = horner_main(lds, h0, w0, c.lk);
+    h1 = horner_main(lds, h1, w1, c.lk);
+    h2 = horner_main(lds, h2, w2, c.lk);
+    h3 = horner_main(lds, h3, w3, c.lk);
+    const uint64_t ends = __builtin_amdgcn_ballot_w64(last && k == 0);
+    if (ends) {
+      if (last) {
+        const uint32_t pos = parked + (uint32_t)__builtin_popcountll(ends & ((1ull << lead) - 1ull));
+        const uint32_t row = (pos >> 3) & 1u, col = pos & 7u;
+        S.park[wv][row][col * 8u + k] = u32x4{h0, h1, h2, h3};
+        if (k == 0) {
+          S.pmeta[wv][row][col][0] = id;
+          S.pmeta[wv][row][col][1] = (f >> kGsZShift) & 3u;
+        }
+        h0 = h1 = h2 = h3 = 0;
+      }
+      const uint32_t before = parked;
+      parked += (uint32_t)__builtin_popcountll(ends);
+      if ((before ^ parked) & ~7u) combine_row((before >> 3) & 1u, 8u);  // a row is full
+    }
+  };
+
+  // ---- main loop ----
+  u32x4 ring[kGsRing];
+  uint32_t rflags[kGsRing], rid[kGsRing];
+#pragma unroll
+  for (int q = 0; q < kGsRing; ++q) produce(ring[q], rflags[q], rid[q]);
+  uint32_t idle_slots = 0;  // consecutive producer steps with every group idle
+  for (;;) {
+    desc_issue();  // this ring cycle's descriptor reload (written at its end)
+#pragma unroll
+    for (int q = 0; q < kGsRing; ++q) {
+      const u32x4 data = ring[q];
+      const uint32_t f = rflags[q], id = rid[q];
+      consume(data, f, id);
+      produce(ring[q], rflags[q], rid[q]);
+      idle_slots = __builtin_amdgcn_ballot_w64(pid != kGsIdle) ? 0u : idle_slots + 1u;
+    }
+    desc_commit();
+    if (idle_slots >= (uint32_t)kGsRing) break;  // every issued step has been consumed
+  }
+  if (parked & 7u) combine_row((parked >> 3) & 1u, parked & 7u);
+}
+
 }  // namespace
 
 int cu_count_for_current_device();
@@ -1359,16 +1647,28 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
   Batch<true> b{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count};
-  if (count < kSortMinPackets || count > 0xFFFFFFFFull) {
+  // Default: the step-class sort + round DMA kernel.  ENET_CRC_RAGGED=groups selects the
+  // group-stream kernel (no pre-pass; bit-exact, but 1.28x slower on G2: DESIGN.md §4),
+  // =stream the register streaming kernel (A/B runs).
+  static const int ragged_mode = [] {
+    const char* v = getenv("ENET_CRC_RAGGED");
+    if (v && strcmp(v, "stream") == 0) return 2;
+    if (v && strcmp(v, "groups") == 0) return 0;
+    return 1;
+  }();
+  if (count > 0xFFFFFFFFull || (ragged_mode != 0 && count < kSortMinPackets)) {
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // Scratch in stream order: histogram, then the permutation or the round
-  // records.  ENET_CRC_RAGGED=stream selects the register streaming kernel (A/B runs).
-  static const bool stream_kernel = [] {
-    const char* v = getenv("ENET_CRC_RAGGED");
-    return v && strcmp(v, "stream") == 0;
-  }();
+  if (ragged_mode == 0) {
+    const uint64_t ntasks = (count + kGsTask - 1) / kGsTask;
+    uint64_t gblocks = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (gblocks > (uint64_t)blocks) gblocks = blocks;
+    const GsBatch gb{b.base, offsets, lengths, count};
+    hipLaunchKernelGGL(crc32_group_stream_kernel, dim3((unsigned)gblocks), dim3(kBlock), 0, stream, gb, out);
+    return hipGetLastError();
+  }
+  const bool stream_kernel = ragged_mode == 2;
   // >= 4096 packets per sort block: every records/scatter block reads the whole
   // histogram (16 x sort_blocks entries) to find its output positions.
   uint64_t sort_blocks = (count + 16 * kSortBlock - 1) / (16 * kSortBlock);
