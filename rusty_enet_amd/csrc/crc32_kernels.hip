@@ -673,6 +673,7 @@ struct UniformBatch {
 // load_top_words only when the chunk would reach below the caller's base.
 // ---------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void LdsVoid;
+typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
 constexpr int kRaggedRing = 4;                               // ragged kernel (its round records need LDS too)
 constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
@@ -1058,7 +1059,10 @@ struct RaggedRound {
   uint32_t id;          // packet id (output index)
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
   bool direct;          // top chunk read directly (not fallback / not before the packet)
+  bool fast;            // wave-uniform: every lane's top is slot 0, no fallback, ns <= kRaggedFastMax
 };
+
+constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
 
 __device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint64_t& addr, uint32_t& len,
                                             uint32_t& id) {
@@ -1071,6 +1075,91 @@ __device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint
       : "=&v"(addr), "=&v"(len), "=&v"(id)
       : "v"(a), "v"(l), "v"(i)
       : "memory");
+}
+
+// Source of this lane's slot-s DMA in round rr (the zero chunk before its top).
+__device__ __forceinline__ uint64_t ragged_src(const RaggedRound& rr, int32_t s, uint64_t dummy) {
+  const bool real = s > rr.top_slot || (s == rr.top_slot && rr.direct);
+  return real ? rr.cb + (uint64_t)kBytesPerStep * (uint64_t)s : dummy;
+}
+
+// Shared state of one wave's LDS-DMA ring (crc32_ragged_dma_kernel).
+struct RaggedRing {
+  LdsVoid* slot0;     // this wave's ring position 0
+  uint32_t ring0;     // its LDS byte address
+  uint32_t lane16;    // lane * 16
+  uint32_t q;         // ring position of the slot being consumed (wave-uniform)
+  u32x4 nextv;        // landed data of the slot about to be consumed
+  __device__ __forceinline__ void dma(uint64_t src) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 0);
+    q = q + 1 == (uint32_t)kRaggedRing ? 0u : q + 1;
+  }
+  __device__ __forceinline__ uint32_t next_addr() const { return ring0 + q * kRingStride + lane16; }
+};
+
+// A round in which every packet has exactly NS steps and needs no fallback: the slot
+// loop of crc32_uniform_dma_kernel (unrolled, lookups fused with the next ring read);
+// slot 0 masks the top words, the last slot the bytes past each packet's end.
+template <int NS>
+__device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
+                                                  const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                                  uint32_t& h3) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const u32x4 v = R.nextv;
+    const int32_t f = s + kRaggedRing;  // refill this slot's LDS slot kRaggedRing slots ahead
+    R.dma(f < NS ? cur.cb + (uint64_t)kBytesPerStep * (uint64_t)f : ragged_src(nxt, f - NS, c.dummy));
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    if (s == NS - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
+    if (s == 0) {
+      if (__builtin_amdgcn_ballot_w64(cur.meta & kMetaHeadMask)) {
+        if (cur.meta & kMetaHeadMask) mask_top(cur.meta, w0, w1, w2, w3);
+      }
+      h0 = w0;  // top step: M32^32(0) = 0, no lookups
+      h1 = w1;
+      h2 = w2;
+      h3 = w3;
+      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
+    } else {
+      horner_step_and_read<kRaggedRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, R.next_addr(), R.nextv);
+    }
+    issue_order_fence();
+  }
+}
+
+template <int... I>
+__device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRound& cur, const RaggedRound& nxt,
+                                                      RaggedRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
+                                                      uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
+  return ((ns == I + kRaggedRing ? (ragged_round_fast<I + kRaggedRing>(cur, nxt, R, c, h0, h1, h2, h3), true)
+                                 : false) || ...);
+}
+
+// Any round (mixed step counts, fallback chunks, long packets): per-lane top slot.
+__device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
+                                                     const LaneConsts& c, const uint32_t* lds, uint32_t& h0,
+                                                     uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  for (int32_t s = 0; s < cur.ns; ++s) {
+    const u32x4 v = R.nextv;
+    const int32_t f = s + kRaggedRing;
+    R.dma(f < cur.ns ? ragged_src(cur, f, c.dummy) : ragged_src(nxt, f - cur.ns, c.dummy));
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    const bool top = s == cur.top_slot;
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
+      if (top && (cur.meta & kMetaFallback))
+        load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
+    }
+    if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
+    }
+    h0 = horner_main(lds, h0, w0, c.lk);
+    h1 = horner_main(lds, h1, w1, c.lk);
+    h2 = horner_main(lds, h2, w2, c.lk);
+    h3 = horner_main(lds, h3, w3, c.lk);
+    R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
+    issue_order_fence();
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch b, uint32_t* __restrict__ out) {
@@ -1092,9 +1181,6 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
   const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
   auto round_of = [&](uint32_t d) -> uint64_t {
     return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
-  };
-  auto dma16 = [&](uint64_t src, uint32_t q) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 0);
   };
   auto dma_record = [&](uint64_t rnd, uint32_t buf) {
     const uint64_t r = rnd < total_rounds ? rnd : total_rounds - 1;
@@ -1121,54 +1207,43 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
     rr.meta = round_meta(g, c.k, c.base4, valid, unused_tail, c.dummy) | (z << kMetaNTailShift);
     rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
     rr.id = id;
+    // Fast: every packet starts at slot 0 (same step count), no fallback chunk, and the
+    // lanes whose top chunk lies before their packet are exactly the ones the round
+    // reads as zeros (ragged_src with top_slot 0 and !direct).
+    rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != 0 || (rr.meta & kMetaFallback)) &&
+              rr.ns <= kRaggedFastMax;
     return rr;
-  };
-  auto unit_src = [&](const RaggedRound& rr, int32_t s) -> uint64_t {
-    const bool real = s > rr.top_slot || (s == rr.top_slot && rr.direct);
-    return real ? rr.cb + (uint64_t)kBytesPerStep * (uint64_t)s : c.dummy;
   };
 
   uint64_t rnd[kLook + 1];
 #pragma unroll
   for (int i = 0; i < kLook; ++i) rnd[i] = round_of(wv + (uint32_t)(kWavesPerBlock * i));
   if (rnd[0] >= total_rounds) return;
+  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
   dma_record(rnd[0], 0);
   dma_record(rnd[1], 1);
   __builtin_amdgcn_s_waitcnt(0);  // prologue only: both records landed (no other LDS-DMA yet)
   RaggedRound cur = make_round(rnd[0], 0);
   RaggedRound nxt = make_round(rnd[1], 1);
   dma_record(rnd[2], 0);  // read one round from now
+  RaggedRing R;
+  R.slot0 = (LdsVoid*)&ring[0][wv][0];
+  R.ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
+  R.lane16 = lane * 16u;
+  R.q = 0;
 #pragma unroll
-  for (int f = 0; f < kDmaRing; ++f) dma16(unit_src(cur, f), (uint32_t)f);  // cur.ns >= kDmaRing
-  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
-  uint32_t q = 0;
+  for (int f = 0; f < kDmaRing; ++f) R.dma(ragged_src(cur, f, c.dummy));  // cur.ns >= kDmaRing
+  R.nextv = read_landed_slot<kDmaRing - 1>(R.next_addr());
   uint32_t res = 0, res_id = 0, j = 0;
   bool res_valid = false;
   while (rnd[0] < total_rounds) {
     uint32_t d = 0;
     if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    for (int32_t s = 0; s < cur.ns; ++s) {
-      const u32x4 v = read_landed_slot<kDmaRing - 1>(ring0 + q * kRingStride + lane * 16u);
-      const int32_t f = s + kDmaRing;
-      dma16(f < cur.ns ? unit_src(cur, f) : unit_src(nxt, f - cur.ns), q);
-      q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
-      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-      const bool top = s == cur.top_slot;
-      if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
-        if (top && (cur.meta & kMetaFallback))
-          load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
-      }
-      if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
-      if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
-        if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
-      }
-      h0 = horner_main(lds, h0, w0, c.lk);
-      h1 = horner_main(lds, h1, w1, c.lk);
-      h2 = horner_main(lds, h2, w2, c.lk);
-      h3 = horner_main(lds, h3, w3, c.lk);
-      issue_order_fence();
-    }
+    if (!cur.fast ||
+        !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
+                               std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing + 1>{}))
+      ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
     // Round end (record rnd[2] has landed: >= kDmaRing-1 DMAs since it was issued).
     uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
@@ -1197,7 +1272,6 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
   }
   __builtin_amdgcn_s_waitcnt(0);
 }
-
 
 // ---------------------------------------------------------------------------------
 // Group-stream kernel: ragged batches in their own order, no pre-pass.
@@ -1647,10 +1721,12 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
   Batch<true> b{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count};
-  // Default: the step-class sort + round DMA kernel.  ENET_CRC_RAGGED=groups selects the
-  // group-stream kernel (no pre-pass; bit-exact, but 1.28x slower on G2: DESIGN.md §4),
-  // =stream the register streaming kernel (A/B runs).
-  static const int ragged_mode = [] {
+  // Default: the whole batch sorted by step class (histogram + records kernels), then
+  // the round DMA kernel.  ENET_CRC_RAGGED=groups selects the group-stream kernel (no
+  // pre-pass; bit-exact, but 1.28x slower on G2: DESIGN.md §4), =stream the register
+  // streaming kernel (A/B runs).
+  // (Read per launch, not cached, so one process can A/B and test every path.)
+  const int ragged_mode = [] {
     const char* v = getenv("ENET_CRC_RAGGED");
     if (v && strcmp(v, "stream") == 0) return 2;
     if (v && strcmp(v, "groups") == 0) return 0;

@@ -1,8 +1,10 @@
 #!/usr/bin/env bash
-# One gpurun call that produces the round's evidence under gpurun_out/<tag>/:
-#   bench_<cfg>.json      full bench line per config (uniform also with CPU baseline + end-to-end)
-#   prof_<cfg>/           rocprofv3 --kernel-trace --stats of the same bench command
-#   pmc_<cfg>/            rocprofv3 --pmc FETCH_SIZE (own pass, kernel trace only)
+# One gpurun call that produces the round's roofline evidence under gpurun_out/<tag>/:
+#   bench_<cfg>.json   the bench line per config (uniform also with CPU baseline + end-to-end)
+#   prof_<cfg>/        rocprofv3 --kernel-trace --stats of the same bench command
+#   pmc_<cfg>/         rocprofv3 --pmc FETCH_SIZE (own pass, kernel trace only)
+#   ipc_<cfg>_<n>/     instruction / cycle counters (own passes) for uniform and ragged
+#   traffic.json       scripts/traffic_summary.py over the above (kernel-source hash inside)
 #   gpurun --timeout 1200 -- bash scripts/gpu_profile_round.sh <tag>
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -10,18 +12,44 @@ TAG="${1:-round}"
 OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd "$ROOT"
-timeout -k 10 600 python bench.py > "$OUT/bench_uniform.json" 2> "$OUT/bench_uniform.err" || exit $?
+timeout -k 10 300 python bench.py > "$OUT/bench_uniform.json" 2> "$OUT/bench_uniform.err" || exit $?
+echo "[profile] uniform bench done" >&2
 for c in ragged large; do
-  timeout -k 10 300 python bench.py --config $c --cpu-seconds 0 --no-e2e > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || exit $?
+  timeout -k 10 200 python bench.py --config $c --cpu-seconds 0 --no-e2e > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || exit $?
+  echo "[profile] $c bench done" >&2
 done
+timeout -k 10 300 python bench.py --config range > "$OUT/bench_range.json" 2> "$OUT/bench_range.err" || exit $?
+echo "[profile] range bench done" >&2
 export TMPDIR=/tmp
 cd /tmp
-for c in uniform ragged large; do
+for c in uniform ragged large range; do
+  steps=20; [ $c = range ] && steps=3
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o run --output-format csv \
-    -- python3 "$ROOT/bench.py" --config $c --steps 20 --warmup 5 --cpu-seconds 0 --no-verify --no-e2e \
+    -- python3 "$ROOT/bench.py" --config $c --steps $steps --warmup 2 --cpu-seconds 0 --no-verify --no-e2e --no-shard \
     > "$OUT/prof_$c.log" 2>&1 || exit $?
+  echo "[profile] $c kernel stats done" >&2
+done
+for c in uniform ragged large; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_$c" -o run --output-format csv \
-    -- python3 "$ROOT/bench.py" --config $c --steps 5 --warmup 1 --cpu-seconds 0 --no-verify --no-e2e \
+    -- python3 "$ROOT/bench.py" --config $c --steps 5 --warmup 1 --cpu-seconds 0 --no-verify --no-e2e --no-shard \
     > "$OUT/pmc_$c.log" 2>&1 || exit $?
+  echo "[profile] $c FETCH_SIZE done" >&2
+done
+i=0
+for counters in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+                "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+                "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  for c in uniform ragged; do
+    timeout -k 10 120 rocprofv3 --kernel-trace --pmc $counters -d "$OUT/ipc_${c}_$i" -o run --output-format csv \
+      -- python3 "$ROOT/bench.py" --config $c --steps 5 --warmup 1 --cpu-seconds 0 --no-verify --no-e2e --no-shard \
+      > "$OUT/ipc_${c}_$i.log" 2>&1 || exit $?
+  done
+  echo "[profile] counter pass $i done" >&2
+done
+cd "$ROOT"
+python3 scripts/traffic_summary.py "gpurun_out/$TAG" > "$OUT/traffic.json" 2>&1 || exit $?
+for c in uniform ragged; do
+  python3 scripts/pmc_summary.py "$OUT"/ipc_${c}_* > "$OUT/ipc_${c}_summary.txt" 2>&1
 done
 echo "[profile] done" >&2

@@ -5,9 +5,10 @@ import os
 import sys
 from collections import defaultdict
 
-root = sys.argv[1]
 acc = defaultdict(lambda: defaultdict(list))
-for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recursive=True):
+paths = [p for root in sys.argv[1:] for p in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"),
+                                                           recursive=True)]
+for path in paths:
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "?")

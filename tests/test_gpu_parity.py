@@ -230,3 +230,24 @@ def test_per_call_65_slices(dev):
     for trial in range(20):
         slices = [splitmix64_bytes(100 * trial + j, int(rng.integers(0, 40)) if j < 9 else 0) for j in range(65)]
         assert rea.crc32(slices) == _oracle.crc32(slices)
+
+
+# --- the alternative ragged kernels (ENET_CRC_RAGGED), same oracle --------------------------
+
+@pytest.mark.parametrize("mode", ["groups", "stream"])
+def test_alternative_ragged_kernels(dev, mode, monkeypatch):
+    monkeypatch.setenv("ENET_CRC_RAGGED", mode)
+    lens, offs, pos = [], [], 0
+    for n in range(0, 300):
+        for a in range(8):
+            pos += a
+            offs.append(pos)
+            lens.append(n)
+            pos += n
+    data = splitmix64_bytes(12, pos + 64)
+    offsets, lengths = np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
+    assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
+    lengths = ragged_lengths(ENET_SEED + 5, 200_000, lo=0, hi=4096)
+    offsets = packed_offsets(lengths) + np.uint64(1)
+    data = splitmix64_bytes(13, int(lengths.sum()) + 8)
+    assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
