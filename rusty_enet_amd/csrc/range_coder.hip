@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "range_coder.hpp"
 
 namespace enet_crc {
@@ -225,17 +227,37 @@ struct Encoder {
   }
 };
 
-// enet_range_coder_compress over one contiguous input (compress.rs:60-462).
-__host__ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t out_lim) {
-  if (len == 0) return 0;  // :79-81 (one slice; a single empty slice codes nothing)
+// enet_range_coder_compress over one contiguous input (compress.rs:60-462), as a
+// resumable per-lane state machine: begin() sets a packet up, step() codes ONE input
+// byte and reports whether the packet is finished (its result in `size`).  The kernel
+// calls step() in a loop and starts the lane's next packet as soon as one finishes,
+// so a lane never idles while the longest packet of its wave is still being coded.
+struct CompressLane {
+  const uint8_t* in;
+  uint32_t pos, len, size;
+  uint8_t* out0;
   Encoder e;
-  e.out = out;
-  e.end = out + out_lim;
-  m.reset();
-  uint32_t nextv = in[0];
-  for (uint32_t pos = 0; pos < len; ++pos) {
-    const uint32_t value = nextv;
-    if (pos + 1 < len) nextv = in[pos + 1];  // issue the next byte's load early
+
+  __host__ __device__ void begin(Model& m, const uint8_t* in_, uint32_t len_, uint8_t* out, uint32_t out_lim) {
+    in = in_;
+    len = len_;
+    pos = 0;
+    size = 0;
+    out0 = out;
+    e.out = out;
+    e.end = out + out_lim;
+    e.low = 0;
+    e.range = ~0u;
+    m.reset();
+  }
+
+  // One input byte; true = the packet is finished and `size` holds compress()'s result.
+  __host__ __device__ bool step(Model& m) {
+    if (pos >= len) {  // :79-81 (one slice; a single empty slice codes nothing)
+      size = 0;
+      return true;
+    }
+    const uint32_t value = in[pos];
     uint32_t parent = ~0u;
     uint32_t ctx = m.predicted;
     bool coded = false;
@@ -248,10 +270,10 @@ __host__ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t 
       uint32_t total = lo16(x.w);
       uint32_t esc = hi16(x.z);
       if (count > 0) {
-        if (!e.put(esc + under, count, total)) return 0;
+        if (!e.put(esc + under, count, total)) return fail();
       } else {
         if (esc > 0 && esc < total)
-          if (!e.put(0, esc, total)) return 0;
+          if (!e.put(0, esc, total)) return fail();
         esc = (esc + kSubEscapeDelta) & 0xFFFF;
         total = (total + kSubEscapeDelta) & 0xFFFF;
         m.words(ctx)[2] = pack(x.z, esc);
@@ -270,20 +292,36 @@ __host__ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t 
       const uint32_t sym = m.update(0, value, kCtxSymbolDelta, under, count);
       m.set_parent(parent, sym);
       const Sym r = m.load(0);
-      if (!e.put(hi16(r.z) + under, count, lo16(r.w))) return 0;
+      if (!e.put(hi16(r.z) + under, count, lo16(r.w))) return fail();
       const uint32_t total = (lo16(r.w) + kCtxSymbolDelta) & 0xFFFF;
       m.words(0)[3] = pack(total, hi16(r.w));
       if (count > 0xff - 2 * kCtxSymbolDelta + kSymbolMinimum || total > kBottom - 0x100)
         m.ctx_rescale(0, 256 * kSymbolMinimum);
     }
     m.advance();
+    if (++pos < len) return false;
+    while (e.low) {  // :452-460
+      if (e.out >= e.end) return fail();
+      *e.out++ = (uint8_t)(e.low >> 24);
+      e.low <<= 8;
+    }
+    size = (uint32_t)(e.out - out0);
+    return true;
   }
-  while (e.low) {  // :452-460
-    if (e.out >= e.end) return 0;
-    *e.out++ = (uint8_t)(e.low >> 24);
-    e.low <<= 8;
+
+  __host__ __device__ bool fail() {  // output limit reached: compress() returns 0
+    size = 0;
+    return true;
   }
-  return (uint32_t)(e.out - out);
+};
+
+[[maybe_unused]] __host__ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t out_lim) {
+  if (len == 0) return 0;  // :79-81
+  CompressLane c;
+  c.begin(m, in, len, out, out_lim);
+  while (!c.step(m)) {
+  }
+  return c.size;
 }
 
 struct Decoder {
@@ -307,18 +345,38 @@ struct Decoder {
   }
 };
 
-// enet_range_coder_decompress (compress.rs:463-987).
-RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t len, uint8_t* out,
-                                                           uint32_t out_lim) {
-  if (len == 0) return 0;  // :481-483
+// enet_range_coder_decompress (compress.rs:463-987) as a resumable per-lane state
+// machine (see CompressLane): step() decodes ONE symbol.
+struct DecompressLane {
   Decoder d;
-  d.in = in;
-  d.end = in + len;
-  m.reset();
-  for (int k = 24; k >= 0; k -= 8)  // :500-519
-    if (d.in < d.end) d.code |= (uint32_t)(*d.in++) << k;
-  uint32_t n = 0;
-  for (;;) {
+  uint8_t* out;
+  uint32_t n, out_lim, size;
+  bool empty;
+
+  __host__ __device__ void begin(Model& m, const uint8_t* in, uint32_t len, uint8_t* out_, uint32_t out_lim_) {
+    d.low = 0;
+    d.code = 0;
+    d.range = ~0u;
+    d.in = in;
+    d.end = in + len;
+    out = out_;
+    out_lim = out_lim_;
+    n = 0;
+    size = 0;
+    empty = len == 0;  // :481-483
+    m.reset();
+    for (int k = 24; k >= 0; k -= 8)  // :500-519
+      if (d.in < d.end) d.code |= (uint32_t)(*d.in++) << k;
+  }
+
+  __host__ __device__ bool finish(uint32_t result) {
+    size = result;
+    return true;
+  }
+
+  // One symbol; true = the packet is finished and `size` holds decompress()'s result.
+  RC_DECODE_ATTR __host__ __device__ bool step(Model& m) {
+    if (empty) return finish(0);
     uint32_t value = 0, bottom = 0;
     uint32_t ctx = m.predicted;
     bool found = false;
@@ -333,7 +391,7 @@ RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8
         } else {
           code = (code - esc) & 0xFFFF;
           uint32_t under = 0, count = 0;
-          if (lo16(x.z) == 0) return RC_FAIL(1, n);
+          if (lo16(x.z) == 0) return finish(RC_FAIL(1, n));
           uint32_t i = ctx + lo16(x.z);
           for (;;) {  // :579-611
             const Sym s = m.load(i);
@@ -341,11 +399,11 @@ RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8
             const uint32_t after = (under + su) & 0xFFFF;
             if (code >= after) {
               under = after;
-              if (!hi16(s.y)) return RC_FAIL(2, n);
+              if (!hi16(s.y)) return finish(RC_FAIL(2, n));
               i += hi16(s.y);
             } else if ((int)code < (int)after - (int)sc) {
               m.words(i)[0] = pack(s.x, su + kSubSymbolDelta);
-              if (!lo16(s.y)) return RC_FAIL(3, n);
+              if (!lo16(s.y)) return finish(RC_FAIL(3, n));
               i += lo16(s.y);
             } else {
               value = sym_value(s);
@@ -372,7 +430,8 @@ RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8
       uint32_t code = ((d.code - d.low) / d.range) & 0xFFFF;
       if (code < hi16(r.z)) {  // end of stream, :674-696
         d.take(0, hi16(r.z));
-        break;
+        size = n;
+        return true;
       }
       code = (code - hi16(r.z)) & 0xFFFF;
       uint32_t under = 0, count = kSymbolMinimum, sym;
@@ -448,11 +507,21 @@ RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8
       p = hi16(x.w);
     }
     m.set_parent(parent, bottom);
-    if (n >= out_lim) return RC_FAIL(4, n);  // :949-954
+    if (n >= out_lim) return finish(RC_FAIL(4, n));  // :949-954
     out[n++] = (uint8_t)value;
     m.advance();
+    return false;
   }
-  return n;
+};
+
+[[maybe_unused]] RC_DECODE_ATTR __host__ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t len, uint8_t* out,
+                                                           uint32_t out_lim) {
+  if (len == 0) return 0;  // :481-483
+  DecompressLane dl;
+  dl.begin(m, in, len, out, out_lim);
+  while (!dl.step(m)) {
+  }
+  return dl.size;
 }
 
 struct RangeBatch {
@@ -468,20 +537,28 @@ struct RangeBatch {
   uint64_t workers;
 };
 
+// One lane = one coder: packets w, w + workers, ... in turn, one symbol per loop trip;
+// a lane whose packet finishes starts its next one on the next trip.
 template <bool kDecompress>
 __global__ __launch_bounds__(kBlock) void range_coder_kernel(RangeBatch b) {
   const uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (w >= b.workers) return;
+  if (w >= b.workers || w >= b.count) return;
   Model m;
   m.a = b.arenas + w * kArena;
   m.next = 0;
   m.predicted = 0;
   m.order = 0;
-  for (uint64_t p = w; p < b.count; p += b.workers) {
-    const uint8_t* in = b.in + b.in_off[p];
-    uint8_t* out = b.out + b.out_off[p];
-    const uint32_t len = b.in_len[p], lim = b.out_lim[p];
-    b.sizes[p] = kDecompress ? decompress_one(m, in, len, out, lim) : compress_one(m, in, len, out, lim);
+  using Lane = typename std::conditional<kDecompress, DecompressLane, CompressLane>::type;
+  Lane lane;
+  uint64_t p = w;
+  lane.begin(m, b.in + b.in_off[p], b.in_len[p], b.out + b.out_off[p], b.out_lim[p]);
+  for (;;) {
+    if (lane.step(m)) {
+      b.sizes[p] = lane.size;
+      p += b.workers;
+      if (p >= b.count) break;
+      lane.begin(m, b.in + b.in_off[p], b.in_len[p], b.out + b.out_off[p], b.out_lim[p]);
+    }
   }
 }
 

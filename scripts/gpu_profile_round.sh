@@ -35,6 +35,10 @@ for c in uniform ragged large; do
     > "$OUT/pmc_$c.log" 2>&1 || exit $?
   echo "[profile] $c FETCH_SIZE done" >&2
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -d "$OUT/pmc_range" -o run --output-format csv \
+  -- python3 "$ROOT/bench.py" --config range --steps 2 --warmup 1 --cpu-seconds 0 --no-verify \
+  > "$OUT/pmc_range.log" 2>&1 || exit $?
+echo "[profile] range read requests done" >&2
 i=0
 for counters in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
                 "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \

@@ -43,7 +43,7 @@ co = torch.from_numpy(c_offs.astype(np.int64)).to(dev)
 cl = torch.from_numpy(c_lens.astype(np.int32)).to(dev)
 dl = torch.from_numpy(lens[keep].astype(np.int32)).to(dev)
 dec_bytes = int(lens[keep].sum())
-for w in (8192, 16384, 32768, 65536, 131072, 262144):
+for w in [int(x) for x in os.environ.get("SWEEP_WORKERS", "8192 16384 32768 65536 131072 262144").split()]:
     for op in ("compress", "decompress"):
         fn = (lambda: rea.compress_batch(data, off, ln, workers=w)) if op == "compress" else \
              (lambda: rea.decompress_batch(cd, co, cl, dl, workers=w))
