@@ -345,6 +345,18 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
             ctx.crc32(pkt)
         variants[name] = round((time.perf_counter() - t0) / calls * 1e6, 2)
     per_call_us = variants["zerocopy"]  # the context's default mode
+    # Floor of any per-call GPU path: one trivial kernel launch + stream synchronize.
+    import torch
+
+    x = torch.zeros(1, device=dev)
+    for _ in range(50):
+        x.add_(1)
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        x.add_(1)
+        torch.cuda.synchronize()
+    floor_us = (time.perf_counter() - t0) / 2000 * 1e6
     # The reference's own per-call cost for the same datagram: the oracle's Sarwate loop on one core.
     t0 = time.perf_counter()
     for _ in range(2000):
@@ -356,8 +368,10 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
             "per_call_us": round(per_call_us, 2),
             "per_call_variants_us": variants,
             "per_call_cpu_oracle_us": round(cpu_call_us, 2),
+            "per_call_floor_us": round(floor_us, 2),
             "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000; "
-                               "cpu: the C restatement of src/crc32.rs on the same datagram through ctypes",
+                               "cpu: the C restatement of src/crc32.rs on the same datagram through ctypes; floor: one "
+                               "trivial torch kernel launch + torch.cuda.synchronize",
             "ring": ring_rate(dev, L)}
 
 
