@@ -45,12 +45,14 @@
 #include <string.h>
 
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "crc32_geometry.hpp"
 #include "crc32_kernels.hpp"
 #include "crc32_layout.hpp"
 #include "crc32_ops.hpp"
+#include "crc32_slot.hpp"
 
 namespace enet_crc {
 
@@ -74,6 +76,7 @@ typedef __attribute__((address_space(1))) const U32x4A4 GlobalU32x4A4;
 constexpr int kBlock = 1024;
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int G = kLanesPerPacket;
+constexpr int kStreamDepth = 8;  // ring depth of the streaming kernel
 // LDS layout constants, Lookup and make_lookup(): crc32_layout.hpp.
 
 __device__ __forceinline__ uint32_t load_word(uint64_t addr) { return *reinterpret_cast<GlobalU32*>(addr); }
@@ -428,11 +431,9 @@ __global__ __launch_bounds__(kBlock) void crc32_rounds_kernel(Batch<kRagged> b, 
 // Streaming kernel: any packet lengths.  Each round (8 packets of a wave) is padded
 // to T = ceil(max nsteps / U) * U slots and streamed through a U-deep ring.
 // ---------------------------------------------------------------------------------
+// The rounds of one wave (`lds` filled by fill_lds); also the flat path's fallback.
 template <int U, bool kRagged>
-__global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
-  fill_lds(lds);
-  __syncthreads();
+__device__ __forceinline__ void stream_rounds(const uint32_t* lds, const Batch<kRagged>& b, uint32_t* __restrict__ out) {
   const LaneConsts c = lane_consts(b.base);
 
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
@@ -491,6 +492,14 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
     }
     finish_round(lds, h0, h1, h2, h3, meta, tail_word, c.k, c.lk, out + packet_id(b, p));
   }
+}
+
+template <int U, bool kRagged>
+__global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
+  fill_lds(lds);
+  __syncthreads();
+  stream_rounds<U, kRagged>(lds, b, out);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1560,12 +1569,471 @@ __global__ __launch_bounds__(kBlock) void crc32_group_stream_kernel(GsBatch batc
   if (parked & 7u) combine_row((parked >> 3) & 1u, parked & 7u);
 }
 
+// ---------------------------------------------------------------------------------
+// Flat-stream ragged kernels (SURVEY.md §7 "Ragged batch": the batch as one byte
+// stream, cut at fixed positions, packets recovered by linearity).  Default for ragged
+// batches whose packets lie in address order without overlap (gaps <= kFlatMaxGap: a
+// packed receive buffer, or fixed receive slots), which crc32_flat_prep_kernel checks
+// on the device; other batches take the streaming kernel inside the finish launch.
+//
+// Geometry (flat_geo).  The stream [lo, hi) is the packets' span rounded out to 128 B,
+// cut into ngroups regions of spg steps of 128 B.  Region r belongs to group r % 8 of
+// wave r / 8, so every group runs exactly spg steps (no load imbalance, no sort) and a
+// wave's LDS-DMA reads 8 x 128 B from 8 neighbouring regions, the uniform kernel's
+// access shape.  Regions tile the stream: no line is read twice.  Lane k of a group
+// holds bytes [112 - 16k, 128 - 16k) of every step (lane 0 the last 16 B: the order
+// combine_streams assumes).
+//
+// Linear prefix.  Each group runs the uniform kernel's step (4 x 8 word streams,
+// h = M32^32(h) ^ w) over its whole region and never resets: its streams hold
+// G_r(x), the zero-initialised CRC register of the region's bytes [R0, x).  At every
+// packet boundary x (each packet's end; its start too after a gap) it combines the
+// streams with the bytes at and after x removed: E(x) = M8^(T - x) G_r(x), T = the end
+// of the step holding x.  At the region's end, tails[r] = G_r(R1).  Since
+// reg(bytes [s, e)) = G(e) ^ M8^(e - s) G(s) ^ M8^(e - s)(init), the finish pass
+// (one thread per packet) gets every checksum from E(e), E(s), the tails of the
+// regions the packet spans (moved by M8^(multiple of 128) through the forward ladder),
+// one inverse shift M8^-(T - e) (< 128 bytes) and a table of M8^len(init).
+// Descriptors reach a group by LDS-DMA in windows of 8 packets (double-buffered),
+// E(end) values leave 8 at a time (one 32-B store per group).
+// ---------------------------------------------------------------------------------
+constexpr int kFlatRing = 4;                       // LDS slots per wave
+constexpr int kFlatPrepBlock = 256;
+constexpr int kFlatPrepRun = 8;                    // consecutive packets per prep thread
+constexpr int kFlatMaxFlags = 1024;                // prep blocks
+constexpr uint32_t kFlatMaxLen = 1u << 28;         // eligibility: packet length
+constexpr uint64_t kFlatMaxGap = 4096;             // eligibility: bytes between neighbours
+constexpr uint64_t kFlatMaxSpg = 1u << 20;         // eligibility: region <= 128 MiB
+constexpr uint32_t kFlatMaxRegionsPerPacket = 64;  // eligibility: bounds a prep thread's work
+constexpr int32_t kFlatFar = 1 << 30;              // position of "no boundary" (past every region)
+constexpr int kFinFwdBase = 5;                     // M32^(32 * 2^i): level 5 + i of the ladder
+constexpr int kFinFwdLds = 8;                      // of which the first 8 are staged in LDS
+
+struct FlatBatch {
+  uint64_t base;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
+  uint64_t count;
+  uint32_t ngroups;        // regions: gridDim.x * 128 of the main kernel
+  uint32_t nflags;         // prep blocks
+  uint32_t* flags;         // [nflags] nonzero: batch not flat-eligible
+  uint32_t* first;         // [ngroups] first packet whose end lies after the region's start
+  uint32_t* tails;         // [ngroups] G_r(R1) of each region
+  uint32_t* e_end;         // [count] E(end of packet)
+  uint32_t* e_start;       // [count] E(start of packet), written only after a gap
+  const uint32_t* ladder;  // device ladder: forward levels, inverse levels, M8^len(init) table
+};
+
+struct FlatGeo {
+  uint64_t lo;      // absolute address of step 0 of region 0
+  uint64_t nsteps;  // steps of the span
+  uint64_t rb;      // bytes per region
+  uint64_t spg;     // steps per region (unclamped: the prep kernel rejects > kFlatMaxSpg)
+};
+
+__device__ __forceinline__ FlatGeo flat_geo(const FlatBatch& b) {
+  const uint64_t s = b.base + b.offsets[0];
+  const uint64_t e = b.base + b.offsets[b.count - 1] + b.lengths[b.count - 1];
+  FlatGeo g;
+  g.lo = s & ~(uint64_t)127;
+  const uint64_t hi = e > g.lo ? (e + 127) & ~(uint64_t)127 : g.lo + 128;
+  g.nsteps = (hi - g.lo) >> 7;
+  g.spg = (g.nsteps + b.ngroups - 1) / b.ngroups;
+  g.rb = (g.spg < kFlatMaxSpg ? g.spg : kFlatMaxSpg) * 128;
+  return g;
+}
+
+// Block-wide: did the prep kernel accept the batch?
+__device__ __forceinline__ bool flat_batch_ok(const FlatBatch& b) {
+  uint32_t bad = 0;
+  for (uint32_t i = threadIdx.x; i < b.nflags; i += blockDim.x) bad |= b.flags[i];
+  return __syncthreads_or(bad) == 0;
+}
+
+// Eligibility (address order, no overlap, gaps <= kFlatMaxGap, lengths < kFlatMaxLen,
+// <= kFlatMaxRegionsPerPacket regions starting inside one packet) and the region map
+// first[r] = min p with end(p) > start(r).  A thread walks kFlatPrepRun consecutive
+// packets and the regions starting in [end(p-1), end(p)) of each (one division per
+// run), so in an eligible batch every entry has exactly one writer.
+__global__ __launch_bounds__(kFlatPrepBlock) void crc32_flat_prep_kernel(FlatBatch b) {
+  const FlatGeo g = flat_geo(b);
+  auto region_ceil = [&](uint64_t rel) -> uint64_t {  // first region starting at or after base + rel
+    const uint64_t x = b.base + rel;
+    if (x <= g.lo) return 0;
+    const uint64_t r = (x - g.lo + g.rb - 1) / g.rb;
+    return r < b.ngroups ? r : b.ngroups;
+  };
+  bool bad = g.spg > kFlatMaxSpg;
+  constexpr uint64_t kPerBlock = (uint64_t)kFlatPrepBlock * kFlatPrepRun;
+  for (uint64_t p0 = (uint64_t)blockIdx.x * kPerBlock + (uint64_t)threadIdx.x * kFlatPrepRun; p0 < b.count && !bad;
+       p0 += (uint64_t)gridDim.x * kPerBlock) {
+    // The run's descriptors, all loads issued before any is used.
+    uint64_t offs[kFlatPrepRun];
+    uint32_t lens[kFlatPrepRun];
+#pragma unroll
+    for (int i = 0; i < kFlatPrepRun; ++i) {
+      const uint64_t q = p0 + i < b.count ? p0 + i : b.count - 1;
+      offs[i] = b.offsets[q];
+      lens[i] = b.lengths[q];
+    }
+    uint64_t prev_end = p0 > 0 ? b.offsets[p0 - 1] + b.lengths[p0 - 1] : 0;
+    uint64_t r = p0 > 0 ? region_ceil(prev_end) : 0;
+    uint64_t r0 = g.lo + r * g.rb;
+#pragma unroll
+    for (int i = 0; i < kFlatPrepRun; ++i) {
+      const uint64_t p = p0 + i;
+      if (p >= b.count || bad) break;
+      const uint64_t ps = offs[i];
+      const uint32_t len = lens[i];
+      const uint64_t pe = ps + len;
+      if (len >= kFlatMaxLen || (p > 0 && (ps < prev_end || ps - prev_end > kFlatMaxGap))) {
+        bad = true;
+        break;
+      }
+      uint32_t n = 0;
+      for (; r < b.ngroups && r0 < b.base + pe; ++r, r0 += g.rb) {
+        if (++n > kFlatMaxRegionsPerPacket) break;
+        b.first[r] = (uint32_t)p;
+      }
+      if (n > kFlatMaxRegionsPerPacket) {
+        bad = true;
+        break;
+      }
+      prev_end = pe;
+    }
+  }
+  // Regions after the last packet's end: no packet.
+  const uint64_t rend = region_ceil(b.offsets[b.count - 1] + b.lengths[b.count - 1]);
+  for (uint64_t r = rend + (uint64_t)blockIdx.x * kFlatPrepBlock + threadIdx.x; r < b.ngroups;
+       r += (uint64_t)gridDim.x * kFlatPrepBlock)
+    b.first[r] = (uint32_t)b.count;
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) b.flags[blockIdx.x] = bad ? 1u : 0u;
+}
+
+struct FlatLds {
+  uint32_t tables[kLdsDwords];
+  u32x4 ring[kFlatRing][kWavesPerBlock][64];
+  uint32_t desc[kWavesPerBlock][2][2][64];  // [wave][window][offset low word | length][8 * group + i]
+};
+static_assert(sizeof(FlatLds) <= 160 * 1024, "LDS");
+
+// XOR of 4 LDS dwords and w, the reads hidden from hipcc (which would otherwise drain
+// every LDS-DMA in flight, vmcnt(0), before each table lookup it cannot tell from the
+// DMA destinations).
+__device__ __forceinline__ uint32_t lds_xor4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t w) {
+  asm volatile(
+      "ds_read_b32 %0, %0\n\t"
+      "ds_read_b32 %1, %1\n\t"
+      "ds_read_b32 %2, %2\n\t"
+      "ds_read_b32 %3, %3\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t"
+      "v_bitop3_b32 %0, %0, %3, %4 bitop3:0x96"
+      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+      : "v"(w)
+      : "memory");
+  return a0;
+}
+
+__device__ __forceinline__ uint32_t apply_rep_asm(uint32_t h, uint32_t w, uint32_t lp, const Lookup& lk) {
+  return lds_xor4(lookup_addr(h, lp, lk, 0), lookup_addr(h, lp, lk, 1), lookup_addr(h, lp, lk, 2),
+                  lookup_addr(h, lp, lk, 3), w);
+}
+
+// M32^n(x) through an unreplicated 4 x 256 table set at LDS byte address `set`.
+__device__ __forceinline__ uint32_t apply_small_asm(uint32_t set, uint32_t x) {
+  return lds_xor4(set + 4u * (x & 0xffu), set + 1024u + 4u * ((x >> 8) & 0xffu), set + 2048u + 4u * ((x >> 16) & 0xffu),
+                  set + 3072u + 4u * (x >> 24), 0u);
+}
+
+// combine_streams with every LDS read in asm (same arithmetic; tables at LDS address 0).
+__device__ __forceinline__ uint32_t combine_streams_asm(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                                        const Lookup& lk) {
+  uint32_t y = apply_rep_asm(h0, h1, lk.lp1, lk);
+  y = apply_rep_asm(y, h2, lk.lp1, lk);
+  y = apply_rep_asm(y, h3, lk.lp1, lk);
+  const uint32_t k = threadIdx.x & (G - 1);
+  constexpr uint32_t tree = 4u * kTreeDword;
+  uint32_t t = 0;
+  if (k & 1u) t = apply_small_asm(tree, y);
+  y ^= from_lane_plus<1>(t);
+  if ((k & 3u) == 2u) t = apply_small_asm(tree + 4096u, y);
+  y ^= from_lane_plus<2>(t);
+  if (k == 4u) t = apply_small_asm(tree + 8192u, y);
+  y ^= from_lane_plus<4>(t);
+  return apply_rep_asm(y, 0u, lk.lp1, lk);
+}
+
+// Bytes of a word below byte index b (b <= 0: none, b >= 4: all).
+__device__ __forceinline__ uint32_t bytes_below(int32_t b) {
+  const uint32_t n = (uint32_t)min(max(b, 0), 4);
+  return n >= 4u ? 0xFFFFFFFFu : (1u << (8u * n)) - 1u;
+}
+
+__global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
+  __shared__ __attribute__((aligned(16))) FlatLds S;
+  if (!flat_batch_ok(b)) return;
+  fill_lds(S.tables);
+  __syncthreads();
+  if ((uint32_t)(uintptr_t)(LdsVoid*)S.tables != 0) __builtin_trap();  // horner_step_and_read addresses
+  const FlatGeo g = flat_geo(b);
+  const LaneConsts c = lane_consts(b.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t region = (blockIdx.x * kWavesPerBlock + wv) * kPacketsPerWave + c.grp;
+  const uint64_t r0 = g.lo + (uint64_t)region * g.rb;  // absolute start of this group's region
+  const uint64_t hi = g.lo + g.nsteps * 128u;
+  const uint32_t spg = (uint32_t)(g.rb >> 7);
+  const int32_t c0 = 112 - 16 * (int32_t)c.k;  // this lane's chunk inside a step
+  const uint32_t r0_lo = (uint32_t)r0, base_lo = (uint32_t)b.base;
+
+  // Data ring (as crc32_uniform_dma_kernel): DMA of step s lands in slot s % kFlatRing.
+  LdsVoid* const slot0 = (LdsVoid*)&S.ring[0][wv][0];
+  const uint32_t ring0 = (uint32_t)(uintptr_t)slot0;
+  uint32_t q = 0;
+  auto dma_step = [&](uint32_t s) {
+    const uint64_t a = r0 + 128ull * s;
+    const uint64_t src = (s < spg && a < hi) ? a + (uint64_t)c0 : c.dummy;
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 0);
+    q = q + 1 == (uint32_t)kFlatRing ? 0u : q + 1;
+  };
+  // Descriptor windows: lane 8g+i of window w holds packet wbase + i of group g.  The
+  // DMAs are asm with their own M0: groups of one wave refill different windows in the
+  // same iteration, and hipcc merges two builtin calls into one whose M0 is the first
+  // active lane's window (readfirstlane), which overwrites other groups' windows.
+  auto dma_desc = [&](auto w_const, uint32_t first_packet) {
+    constexpr uint32_t w = decltype(w_const)::value;
+    uint64_t p = (uint64_t)first_packet + c.k;
+    p = p < b.count ? p : b.count - 1;
+    const uint64_t src_off = (uint64_t)(uintptr_t)(b.offsets + p), src_len = (uint64_t)(uintptr_t)(b.lengths + p);
+    const uint32_t m_off = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LdsVoid*)&S.desc[wv][w][0][0]);
+    const uint32_t m_len = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LdsVoid*)&S.desc[wv][w][1][0]);
+    uint32_t saved_m0;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "global_load_lds_dword %2, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved_m0)
+        : "v"(src_off), "v"(src_len), "s"(m_off), "s"(m_len)
+        : "memory");
+  };
+  const uint32_t desc_lds = (uint32_t)(uintptr_t)(LdsVoid*)&S.desc[wv][0][0][0] + 4u * kLanesPerPacket * c.grp;
+  uint32_t p = region == 0 ? 0u : b.first[region];  // region 0 also takes empty packets at lo
+  auto read_desc = [&](uint32_t w, uint32_t i, int32_t& ps, int32_t& pe) {  // packet p: window w, entry i
+    uint32_t olo, len;
+    const uint32_t a = desc_lds + 512u * w + 4u * i;
+    asm volatile(
+        "ds_read_b32 %0, %2\n\t"
+        "ds_read_b32 %1, %2 offset:256\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(olo), "=&v"(len)
+        : "v"(a)
+        : "memory");
+    const bool valid = p < b.count;
+    ps = valid ? (int32_t)(olo + base_lo - r0_lo) : kFlatFar;
+    pe = valid ? ps + (int32_t)len : kFlatFar;
+  };
+
+  uint32_t wbase = p, cw = 0, win_ready = 0;
+  dma_desc(std::integral_constant<uint32_t, 0>{}, wbase);
+  dma_desc(std::integral_constant<uint32_t, 1>{}, wbase + 8u);
+  __builtin_amdgcn_s_waitcnt(0);  // prologue: both windows landed (vmcnt 0)
+  int32_t ps, pe;
+  read_desc(0, 0, ps, pe);
+  // Next boundary: this packet's start if it lies inside the region (after a gap),
+  // else its end.
+  bool start_pending = ps > 0 && ps < kFlatFar;
+  int32_t xn = start_pending ? ps : pe;
+#pragma unroll
+  for (int f = 0; f < kFlatRing; ++f) dma_step((uint32_t)f);
+  u32x4 nextv = read_landed_slot<kFlatRing - 1>(ring0 + lane * 16u);
+
+  // Boundary values wait in one park slot per group (4 stream words per lane and the
+  // destination) and are combined for all groups at once when some group needs the slot
+  // again: one combine pass serves several groups instead of one pass per boundary.
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+  uint32_t pv0 = 0, pv1 = 0, pv2 = 0, pv3 = 0;
+  uint32_t* pdst = nullptr;  // destination of the parked value (null: slot empty)
+  auto flush = [&]() {       // wave-uniform call
+    const uint32_t E = combine_streams_asm(pv0, pv1, pv2, pv3, c.lk);  // lane k == 0
+    if (pdst != nullptr && c.k == 0) *pdst = E;
+    pdst = nullptr;
+  };
+  for (uint32_t s = 0; s < spg; ++s) {
+    const u32x4 v = nextv;
+    dma_step(s + kFlatRing);
+    const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
+    uint32_t x0 = h0, x1 = h1, x2 = h2, x3 = h3;  // -> M32^32(h) ^ w
+    horner_step_and_read<kFlatRing - 1>(c.lk, x0, x1, x2, x3, v.x, v.y, v.z, v.w, next_addr, nextv);
+    issue_order_fence();
+    h0 = x0;
+    h1 = x1;
+    h2 = x2;
+    h3 = x3;
+    const int32_t S0 = 128 * (int32_t)s;
+    // Boundaries in (S0, S0 + 128]: park the streams without this step's bytes >= x.
+    while (__builtin_amdgcn_ballot_w64(xn <= S0 + 128)) {
+      const bool act = xn <= S0 + 128;
+      if (__builtin_amdgcn_ballot_w64(act && pdst != nullptr)) flush();
+      if (act) {
+        const int32_t B = xn - S0 - c0;
+        pv0 = x0 ^ (v.x & ~bytes_below(B));
+        pv1 = x1 ^ (v.y & ~bytes_below(B - 4));
+        pv2 = x2 ^ (v.z & ~bytes_below(B - 8));
+        pv3 = x3 ^ (v.w & ~bytes_below(B - 12));
+        if (start_pending) {
+          pdst = b.e_start + p;
+          start_pending = false;
+          xn = pe;
+        } else {
+          pdst = b.e_end + p;
+          ++p;
+          if (p - wbase == 8u) {  // window used up: switch windows, refill the other one
+            wbase += 8u;
+            cw ^= 1u;
+            if (s < win_ready) __builtin_amdgcn_s_waitcnt(0);  // the other window's DMA may be in flight
+            if (cw == 1u) dma_desc(std::integral_constant<uint32_t, 0>{}, wbase + 8u);
+            if (cw == 0u) dma_desc(std::integral_constant<uint32_t, 1>{}, wbase + 8u);
+            win_ready = s + (uint32_t)kFlatRing + 1u;
+          }
+          const int32_t prev_end = pe;
+          read_desc(cw, p - wbase, ps, pe);
+          start_pending = ps != prev_end && ps < kFlatFar;
+          xn = start_pending ? ps : pe;
+        }
+      }
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(pdst != nullptr)) flush();
+  {
+    const uint32_t t = combine_streams_asm(h0, h1, h2, h3, c.lk);  // G_r(R1)
+    if (c.k == 0) b.tails[region] = t;
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the ring's last DMAs land before the wave's LDS goes away
+}
+
+// One launch after the main kernel.  Eligible batch: one thread per packet turns the
+// boundary values into checksums.  Otherwise: the streaming kernel's rounds (every
+// packet from scratch; `sb` describes the batch).
+__global__ __launch_bounds__(kBlock) void crc32_flat_finish_kernel(FlatBatch b, Batch<true> sb,
+                                                                   uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
+  if (!flat_batch_ok(b)) {
+    fill_lds(lds);
+    __syncthreads();
+    stream_rounds<kStreamDepth, true>(lds, sb, out);
+    return;
+  }
+  // LDS: forward levels 5..5+kFinFwdLds-1, kInvLevels inverse levels, CRC table, inv_top.
+  uint32_t* const fwd = lds;
+  uint32_t* const inv = lds + kFinFwdLds * kSlotLevelDwords;
+  uint32_t* const crc_table = inv + kInvLevels * kSlotLevelDwords;
+  uint8_t* const inv_top = reinterpret_cast<uint8_t*>(crc_table + 256);
+  static_assert((kFinFwdLds + kInvLevels) * kSlotLevelDwords + 256 + 64 <= kLdsDwords, "finish LDS");
+  const uint32_t* inv_g = b.ladder + kSlotLevels * kSlotLevelDwords;
+  const uint32_t* init_tab = inv_g + kInvLevels * kSlotLevelDwords;
+  {  // every load issued before the first store (one memory latency, not one per level)
+    static_assert(kSlotLevelDwords == kBlock, "one dword per thread per level");
+    uint32_t f[kFinFwdLds], iv[kInvLevels];
+#pragma unroll
+    for (int i = 0; i < kFinFwdLds; ++i) f[i] = b.ladder[(kFinFwdBase + i) * kSlotLevelDwords + threadIdx.x];
+#pragma unroll
+    for (int i = 0; i < kInvLevels; ++i) iv[i] = inv_g[i * kSlotLevelDwords + threadIdx.x];
+    const uint32_t ct = threadIdx.x < 256u ? g_op_tables.sarwate[threadIdx.x] : 0u;
+    const uint8_t it = threadIdx.x < 256u ? g_op_tables.inv_top[threadIdx.x] : 0u;
+#pragma unroll
+    for (int i = 0; i < kFinFwdLds; ++i) fwd[i * kSlotLevelDwords + threadIdx.x] = f[i];
+#pragma unroll
+    for (int i = 0; i < kInvLevels; ++i) inv[i * kSlotLevelDwords + threadIdx.x] = iv[i];
+    if (threadIdx.x < 256u) {
+      crc_table[threadIdx.x] = ct;
+      inv_top[threadIdx.x] = it;
+    }
+  }
+  __syncthreads();
+  const FlatGeo g = flat_geo(b);
+  // x -> M8^(128 m)(x) = M32^(32 m)(x): LDS levels first, global ones for large m.
+  auto fwd_steps = [&](uint32_t x, uint64_t m) {
+#pragma unroll
+    for (int i = 0; i < kFinFwdLds; ++i)
+      if ((m >> i) & 1u) x = ladder_apply(fwd + i * kSlotLevelDwords, x);
+    m >>= kFinFwdLds;
+    for (int i = kFinFwdLds; m != 0; ++i, m >>= 1)
+      if (m & 1u) x = ladder_apply(b.ladder + (kFinFwdBase + i) * kSlotLevelDwords, x);
+    return x;
+  };
+  // Region index of a boundary at absolute address x > lo: the region with R0 < x <= R1.
+  const bool small_span = g.nsteps * 128u < (1ull << 32);
+  const uint32_t rb32 = (uint32_t)g.rb;
+  auto region_of = [&](uint64_t x) -> uint64_t {
+    return small_span ? (uint64_t)((uint32_t)(x - g.lo - 1) / rb32) : (x - g.lo - 1) / g.rb;
+  };
+  // Inputs of one packet; the next packet's are loaded before this one is computed.
+  struct In {
+    uint64_t off, prev_end;
+    uint32_t len, ee, eprev, es, iv;
+  };
+  auto load_in = [&](uint64_t p, In& in) {
+    in.len = b.lengths[p];
+    in.off = b.offsets[p];
+    in.prev_end = p > 0 ? b.offsets[p - 1] + b.lengths[p - 1] : ~(uint64_t)0;
+    in.ee = b.e_end[p];
+    in.eprev = p > 0 ? b.e_end[p - 1] : 0u;
+    in.es = b.e_start[p];  // meaningful only after a gap
+    in.iv = init_tab[in.len < kInitTabLen ? in.len : 0u];
+  };
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  In nx{};
+  if (p < b.count) load_in(p, nx);
+  for (; p < b.count; p += stride) {
+    const In in = nx;
+    if (p + stride < b.count) load_in(p + stride, nx);
+    const uint64_t sa = b.base + in.off, ea = sa + in.len;
+    if (ea <= g.lo) {  // an empty packet at lo
+      out[p] = 0u;
+      continue;
+    }
+    const uint64_t te = (ea + 127u) & ~(uint64_t)127;  // end of the step holding the end boundary
+    uint32_t reg = in.ee;
+    // Tails of the regions from the one holding the start boundary to the one before the end's.
+    const uint64_t rs = sa > g.lo ? region_of(sa) : 0, re = region_of(ea);
+    for (uint64_t r = rs; r < re; ++r) reg ^= fwd_steps(b.tails[r], (te - (g.lo + (r + 1) * g.rb)) >> 7);
+    if (sa > g.lo) {  // E(start): the previous packet's end value when they touch
+      const uint32_t es = b.base + in.prev_end == sa ? in.eprev : in.es;
+      reg ^= fwd_steps(es, (te - ((sa + 127u) & ~(uint64_t)127)) >> 7);
+    }
+    // M8^-(te - ea): < 32 words through the inverse levels, then < 4 bytes.
+    const uint32_t u = (uint32_t)(te - ea);
+    uint32_t wq = u >> 2;
+    for (int k = 0; wq != 0; ++k, wq >>= 1)
+      if (wq & 1u) reg = ladder_apply(inv + k * kSlotLevelDwords, reg);
+    for (uint32_t t = 0; t < (u & 3u); ++t) {
+      const uint32_t idx = inv_top[reg >> 24];
+      reg = ((reg ^ crc_table[idx]) << 8) | idx;
+    }
+    // Initial register: M8^len(0xFFFFFFFF).
+    uint32_t iv = in.iv;
+    if (in.len >= kInitTabLen) {
+      iv = kInitRegister;
+      for (uint32_t t = 0; t < (in.len & 3u); ++t) iv = (iv >> 8) ^ crc_table[iv & 0xffu];
+      uint32_t m = in.len >> 2;
+      for (int k = 0; m != 0; ++k, m >>= 1)
+        if (m & 1u) iv = ladder_apply(b.ladder + k * kSlotLevelDwords, iv);
+    }
+    out[p] = __builtin_bswap32(~(reg ^ iv));
+  }
+}
+
 }  // namespace
 
 int cu_count_for_current_device();
 
 constexpr int kMaxRoundSteps = 14;  // NS 1..14 (packets up to 1792 B); NS >= 15 exceeds 128 VGPRs
-constexpr int kStreamDepth = 8;
 
 template <bool kRagged>
 struct Launcher {
@@ -1722,14 +2190,19 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   if (err != hipSuccess) return err;
   Batch<true> b{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count};
   // Default: the whole batch sorted by step class (histogram + records kernels), then
-  // the round DMA kernel.  ENET_CRC_RAGGED=groups selects the group-stream kernel (no
-  // pre-pass; bit-exact, but 1.28x slower on G2: DESIGN.md §4), =stream the register
-  // streaming kernel (A/B runs).
+  // the round DMA kernel.  ENET_CRC_RAGGED=flat: the flat-stream kernels (prep, main,
+  // finish; the finish launch runs the streaming kernel's rounds for a batch the prep
+  // kernel refused); =flatonly the same WITHOUT the fallback rounds (tests and A/B runs
+  // on batches known to be in address order; any other batch leaves `out` undefined);
+  // =groups the group-stream kernel (no pre-pass; bit-exact, but 1.28x slower on G2:
+  // DESIGN.md §4); =stream the streaming kernel after the sort.
   // (Read per launch, not cached, so one process can A/B and test every path.)
   const int ragged_mode = [] {
     const char* v = getenv("ENET_CRC_RAGGED");
     if (v && strcmp(v, "stream") == 0) return 2;
     if (v && strcmp(v, "groups") == 0) return 0;
+    if (v && strcmp(v, "flat") == 0) return 3;
+    if (v && strcmp(v, "flatonly") == 0) return 4;
     return 1;
   }();
   if (count > 0xFFFFFFFFull || (ragged_mode != 0 && count < kSortMinPackets)) {
@@ -1745,6 +2218,40 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     return hipGetLastError();
   }
   const bool stream_kernel = ragged_mode == 2;
+  if (ragged_mode >= 3) {
+    // Flat path: prep, main, finish (whose blocks run the streaming kernel's rounds
+    // instead when the prep kernel refused the batch).  Regions = groups of the main
+    // kernel's grid (128 per workgroup, at most one workgroup per CU, about two packets
+    // per group at least).
+    uint64_t ngroups = ((count / 2 + 127) / 128) * 128;
+    const uint64_t max_groups = (uint64_t)blocks * kWavesPerBlock * kPacketsPerWave;
+    ngroups = ngroups < 128 ? 128 : (ngroups > max_groups ? max_groups : ngroups);
+    constexpr uint64_t kPrepPer = (uint64_t)kFlatPrepBlock * kFlatPrepRun;
+    uint64_t nflags = (count + kPrepPer - 1) / kPrepPer;
+    nflags = nflags < kFlatMaxFlags ? nflags : kFlatMaxFlags;
+    const uint32_t* ladder = nullptr;
+    err = device_slot_ladder(&ladder);
+    if (err != hipSuccess) return err;
+    void* scratch = nullptr;
+    hipMemPool_t pool = nullptr;
+    err = scratch_pool(&pool);
+    if (err != hipSuccess) return err;
+    const size_t words = (size_t)kFlatMaxFlags + 2 * ngroups + 2 * count;
+    err = hipMallocFromPoolAsync(&scratch, words * 4, pool, stream);
+    if (err != hipSuccess) return err;
+    uint32_t* fs = static_cast<uint32_t*>(scratch);
+    const FlatBatch fb{b.base, offsets, lengths, count, (uint32_t)ngroups, (uint32_t)nflags, fs,
+                       fs + kFlatMaxFlags, fs + kFlatMaxFlags + ngroups, fs + kFlatMaxFlags + 2 * ngroups,
+                       fs + kFlatMaxFlags + 2 * ngroups + count, ladder};
+    Batch<true> sb = b;
+    if (ragged_mode == 4) sb.count = 0;  // ENET_CRC_RAGGED=flatonly: no fallback rounds
+    hipLaunchKernelGGL(crc32_flat_prep_kernel, dim3((unsigned)nflags), dim3(kFlatPrepBlock), 0, stream, fb);
+    hipLaunchKernelGGL(crc32_flat_kernel, dim3((unsigned)(ngroups / 128)), dim3(kBlock), 0, stream, fb);
+    hipLaunchKernelGGL(crc32_flat_finish_kernel, dim3(blocks), dim3(kBlock), 0, stream, fb, sb, out);
+    err = hipGetLastError();
+    const hipError_t ferr = hipFreeAsync(scratch, stream);
+    return err != hipSuccess ? err : ferr;
+  }
   // >= 4096 packets per sort block: every records/scatter block reads the whole
   // histogram (16 x sort_blocks entries) to find its output positions.
   uint64_t sort_blocks = (count + 16 * kSortBlock - 1) / (16 * kSortBlock);

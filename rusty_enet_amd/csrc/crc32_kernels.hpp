@@ -28,6 +28,10 @@ hipError_t launch_slot_fixup(bool insert, uint8_t* base, const uint64_t* offsets
                              const uint32_t* slot_offsets, const uint32_t* slot_values, uint64_t count,
                              uint32_t* crc, uint32_t* ok, const uint32_t* ladder, hipStream_t stream);
 
+// Device copy of the operator ladder (crc32_slot.hpp: build_slot_ladder, then
+// build_inverse_ladder) for the calling thread's device, uploaded on first use.
+hipError_t device_slot_ladder(const uint32_t** out);
+
 // Cached hipDeviceAttributeMultiprocessorCount of the calling thread's device.
 int cu_count_for_current_device();
 

@@ -45,6 +45,48 @@ inline void build_slot_ladder(uint32_t* ladder) {
   }
 }
 
+// Inverse levels (after the kSlotLevels forward levels of the same device buffer):
+// inv[k * 1024 + t * 256 + b] = M32^-(2^k)(b << 8t), k < kInvLevels, which undo up to
+// 4 * (2^kInvLevels - 1) zero bytes (the flat ragged kernel's step-end alignment: <= 128).
+// M8^-1(y) = ((y ^ T[b]) << 8) | b with b = inv_top[y >> 24] (crc32_ops.hpp).
+constexpr int kInvLevels = 6;
+constexpr int kLadderLevels = kSlotLevels + kInvLevels;
+
+inline void build_inverse_ladder(uint32_t* inv) {
+  const OpTables& T = kOpTables;
+  auto m8inv = [&](uint32_t y) {
+    const uint32_t b = T.inv_top[y >> 24];
+    return ((y ^ T.sarwate[b]) << 8) | b;
+  };
+  for (int t = 0; t < 4; ++t)
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t x = b << (8 * t);
+      for (int i = 0; i < 4; ++i) x = m8inv(x);
+      inv[t * 256 + b] = x;
+    }
+  for (int k = 1; k < kInvLevels; ++k) {
+    const uint32_t* prev = inv + (k - 1) * 1024;
+    auto apply_prev = [&](uint32_t x) {
+      return prev[x & 0xffu] ^ prev[256 + ((x >> 8) & 0xffu)] ^ prev[512 + ((x >> 16) & 0xffu)] ^ prev[768 + (x >> 24)];
+    };
+    for (int t = 0; t < 4; ++t)
+      for (uint32_t b = 0; b < 256; ++b) inv[k * 1024 + t * 256 + b] = apply_prev(apply_prev(b << (8 * t)));
+  }
+}
+
+// After the inverse levels: init[len] = M8^len(0xFFFFFFFF) for len < kInitTabLen (the
+// initial register's share of a len-byte packet's register; flat ragged kernels).
+constexpr uint32_t kInitTabLen = 1u << 16;
+constexpr size_t kLadderDwords = (size_t)kLadderLevels * kSlotLevelDwords + kInitTabLen;
+
+inline void build_init_table(uint32_t* t) {
+  uint32_t v = kInitRegister;
+  for (uint32_t n = 0; n < kInitTabLen; ++n) {
+    t[n] = v;
+    v = (v >> 8) ^ kOpTables.sarwate[v & 0xffu];
+  }
+}
+
 ENET_HD uint32_t ladder_apply(const uint32_t* level, uint32_t x) {
   return level[x & 0xffu] ^ level[256 + ((x >> 8) & 0xffu)] ^ level[512 + ((x >> 16) & 0xffu)] ^ level[768 + (x >> 24)];
 }

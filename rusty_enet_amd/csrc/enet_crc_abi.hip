@@ -83,12 +83,15 @@ int stream_device(hipStream_t s) {
 
 }  // namespace
 
-// Operator ladder of the slot correction (crc32_slot.hpp): one host copy, one device
-// copy per device (uploaded on first use, never freed: 128 KiB).
+// Operator ladder of the slot correction and the flat ragged kernel's finish pass
+// (crc32_slot.hpp: kSlotLevels forward + kInvLevels inverse levels + the M8^len(init) table): one host copy, one
+// device copy per device (uploaded on first use, never freed: 408 KiB).
 const uint32_t* host_slot_ladder() {
   static uint32_t* ladder = [] {
-    uint32_t* l = new uint32_t[kSlotLevels * kSlotLevelDwords];
+    uint32_t* l = new uint32_t[kLadderDwords];
     build_slot_ladder(l);
+    build_inverse_ladder(l + kSlotLevels * kSlotLevelDwords);
+    build_init_table(l + kLadderLevels * kSlotLevelDwords);
     return l;
   }();
   return ladder;
@@ -104,7 +107,7 @@ hipError_t device_slot_ladder(const uint32_t** out) {
   if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lk(g_ladder_lock);
   if (!g_device_ladder[dev]) {
-    const size_t bytes = sizeof(uint32_t) * kSlotLevels * kSlotLevelDwords;
+    const size_t bytes = sizeof(uint32_t) * kLadderDwords;
     uint32_t* d = nullptr;
     e = hipMalloc((void**)&d, bytes);
     if (e != hipSuccess) return e;
