@@ -1599,7 +1599,6 @@ __global__ __launch_bounds__(kBlock) void crc32_group_stream_kernel(GsBatch batc
 // ---------------------------------------------------------------------------------
 constexpr int kFlatRing = 4;                       // LDS slots per wave
 constexpr int kFlatPrepBlock = 256;
-constexpr int kFlatPrepRun = 8;                    // consecutive packets per prep thread
 constexpr int kFlatMaxFlags = 1024;                // prep blocks
 constexpr uint32_t kFlatMaxLen = 1u << 28;         // eligibility: packet length
 constexpr uint64_t kFlatMaxGap = 4096;             // eligibility: bytes between neighbours
@@ -1652,60 +1651,37 @@ __device__ __forceinline__ bool flat_batch_ok(const FlatBatch& b) {
 
 // Eligibility (address order, no overlap, gaps <= kFlatMaxGap, lengths < kFlatMaxLen,
 // <= kFlatMaxRegionsPerPacket regions starting inside one packet) and the region map
-// first[r] = min p with end(p) > start(r).  A thread walks kFlatPrepRun consecutive
-// packets and the regions starting in [end(p-1), end(p)) of each (one division per
-// run), so in an eligible batch every entry has exactly one writer.
+// first[r] = min p with end(p) > start(r): packet p (one thread, coalesced loads) writes
+// the regions whose start lies in [end(p-1), end(p)), so in an eligible batch every
+// entry has exactly one writer.  flags[block] = 1 if any packet of the block fails.
 __global__ __launch_bounds__(kFlatPrepBlock) void crc32_flat_prep_kernel(FlatBatch b) {
   const FlatGeo g = flat_geo(b);
+  const bool small = g.nsteps * 128u + g.rb < (1ull << 32);  // 32-bit divisions suffice
+  const uint32_t rb32 = (uint32_t)g.rb;
   auto region_ceil = [&](uint64_t rel) -> uint64_t {  // first region starting at or after base + rel
     const uint64_t x = b.base + rel;
     if (x <= g.lo) return 0;
-    const uint64_t r = (x - g.lo + g.rb - 1) / g.rb;
+    const uint64_t d = x - g.lo;
+    const uint64_t r = small ? (uint64_t)(((uint32_t)d + rb32 - 1u) / rb32) : (d + g.rb - 1) / g.rb;
     return r < b.ngroups ? r : b.ngroups;
   };
   bool bad = g.spg > kFlatMaxSpg;
-  constexpr uint64_t kPerBlock = (uint64_t)kFlatPrepBlock * kFlatPrepRun;
-  for (uint64_t p0 = (uint64_t)blockIdx.x * kPerBlock + (uint64_t)threadIdx.x * kFlatPrepRun; p0 < b.count && !bad;
-       p0 += (uint64_t)gridDim.x * kPerBlock) {
-    // The run's descriptors, all loads issued before any is used.
-    uint64_t offs[kFlatPrepRun];
-    uint32_t lens[kFlatPrepRun];
-#pragma unroll
-    for (int i = 0; i < kFlatPrepRun; ++i) {
-      const uint64_t q = p0 + i < b.count ? p0 + i : b.count - 1;
-      offs[i] = b.offsets[q];
-      lens[i] = b.lengths[q];
-    }
-    uint64_t prev_end = p0 > 0 ? b.offsets[p0 - 1] + b.lengths[p0 - 1] : 0;
-    uint64_t r = p0 > 0 ? region_ceil(prev_end) : 0;
-    uint64_t r0 = g.lo + r * g.rb;
-#pragma unroll
-    for (int i = 0; i < kFlatPrepRun; ++i) {
-      const uint64_t p = p0 + i;
-      if (p >= b.count || bad) break;
-      const uint64_t ps = offs[i];
-      const uint32_t len = lens[i];
-      const uint64_t pe = ps + len;
-      if (len >= kFlatMaxLen || (p > 0 && (ps < prev_end || ps - prev_end > kFlatMaxGap))) {
-        bad = true;
-        break;
-      }
-      uint32_t n = 0;
-      for (; r < b.ngroups && r0 < b.base + pe; ++r, r0 += g.rb) {
-        if (++n > kFlatMaxRegionsPerPacket) break;
-        b.first[r] = (uint32_t)p;
-      }
-      if (n > kFlatMaxRegionsPerPacket) {
-        bad = true;
-        break;
-      }
-      prev_end = pe;
-    }
+  const uint64_t stride = (uint64_t)gridDim.x * kFlatPrepBlock;
+  for (uint64_t p = (uint64_t)blockIdx.x * kFlatPrepBlock + threadIdx.x; p < b.count; p += stride) {
+    const uint64_t ps = b.offsets[p];
+    const uint32_t len = b.lengths[p];
+    const uint64_t pe = ps + len;
+    const uint64_t prev_end = p > 0 ? b.offsets[p - 1] + b.lengths[p - 1] : 0;
+    bool ok = len < kFlatMaxLen && (p == 0 || (ps >= prev_end && ps - prev_end <= kFlatMaxGap));
+    const uint64_t rlo = p > 0 ? region_ceil(prev_end) : 0, rhi = region_ceil(pe);
+    ok = ok && (rhi <= rlo || rhi - rlo <= kFlatMaxRegionsPerPacket);
+    if (ok)
+      for (uint64_t r = rlo; r < rhi; ++r) b.first[r] = (uint32_t)p;
+    bad = bad || !ok;
   }
   // Regions after the last packet's end: no packet.
   const uint64_t rend = region_ceil(b.offsets[b.count - 1] + b.lengths[b.count - 1]);
-  for (uint64_t r = rend + (uint64_t)blockIdx.x * kFlatPrepBlock + threadIdx.x; r < b.ngroups;
-       r += (uint64_t)gridDim.x * kFlatPrepBlock)
+  for (uint64_t r = rend + (uint64_t)blockIdx.x * kFlatPrepBlock + threadIdx.x; r < b.ngroups; r += stride)
     b.first[r] = (uint32_t)b.count;
   bad = __syncthreads_or(bad);
   if (threadIdx.x == 0) b.flags[blockIdx.x] = bad ? 1u : 0u;
@@ -1765,17 +1741,15 @@ __device__ __forceinline__ uint32_t combine_streams_asm(uint32_t h0, uint32_t h1
   return apply_rep_asm(y, 0u, lk.lp1, lk);
 }
 
-// Bytes of a word below byte index b (b <= 0: none, b >= 4: all).
-__device__ __forceinline__ uint32_t bytes_below(int32_t b) {
-  const uint32_t n = (uint32_t)min(max(b, 0), 4);
-  return n >= 4u ? 0xFFFFFFFFu : (1u << (8u * n)) - 1u;
-}
-
-__global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
+__global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b, Batch<true> sb, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) FlatLds S;
-  if (!flat_batch_ok(b)) return;
+  const bool ok = flat_batch_ok(b);
   fill_lds(S.tables);
   __syncthreads();
+  if (!ok) {  // not flat-eligible: the streaming kernel's rounds (same grid, same tables)
+    stream_rounds<kStreamDepth, true>(S.tables, sb, out);
+    return;
+  }
   if ((uint32_t)(uintptr_t)(LdsVoid*)S.tables != 0) __builtin_trap();  // horner_step_and_read addresses
   const FlatGeo g = flat_geo(b);
   const LaneConsts c = lane_consts(b.base);
@@ -1792,9 +1766,11 @@ __global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
   LdsVoid* const slot0 = (LdsVoid*)&S.ring[0][wv][0];
   const uint32_t ring0 = (uint32_t)(uintptr_t)slot0;
   uint32_t q = 0;
+  // Steps of this region that hold stream bytes (the last regions may reach past hi).
+  const uint32_t valid_steps = r0 >= hi ? 0u : (uint32_t)min((uint64_t)spg, (hi - r0) >> 7);
+  const uint64_t src0 = r0 + (uint64_t)c0;
   auto dma_step = [&](uint32_t s) {
-    const uint64_t a = r0 + 128ull * s;
-    const uint64_t src = (s < spg && a < hi) ? a + (uint64_t)c0 : c.dummy;
+    const uint64_t src = s < valid_steps ? src0 + 128ull * s : c.dummy;
     __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 0);
     q = q + 1 == (uint32_t)kFlatRing ? 0u : q + 1;
   };
@@ -1823,7 +1799,7 @@ __global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
   };
   const uint32_t desc_lds = (uint32_t)(uintptr_t)(LdsVoid*)&S.desc[wv][0][0][0] + 4u * kLanesPerPacket * c.grp;
   uint32_t p = region == 0 ? 0u : b.first[region];  // region 0 also takes empty packets at lo
-  auto read_desc = [&](uint32_t w, uint32_t i, int32_t& ps, int32_t& pe) {  // packet p: window w, entry i
+  auto read_desc = [&](uint32_t pk, uint32_t w, uint32_t i, int32_t& ps, int32_t& pe) {  // packet pk: window w, entry i
     uint32_t olo, len;
     const uint32_t a = desc_lds + 512u * w + 4u * i;
     asm volatile(
@@ -1833,7 +1809,7 @@ __global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
         : "=&v"(olo), "=&v"(len)
         : "v"(a)
         : "memory");
-    const bool valid = p < b.count;
+    const bool valid = pk < b.count;
     ps = valid ? (int32_t)(olo + base_lo - r0_lo) : kFlatFar;
     pe = valid ? ps + (int32_t)len : kFlatFar;
   };
@@ -1843,7 +1819,7 @@ __global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
   dma_desc(std::integral_constant<uint32_t, 1>{}, wbase + 8u);
   __builtin_amdgcn_s_waitcnt(0);  // prologue: both windows landed (vmcnt 0)
   int32_t ps, pe;
-  read_desc(0, 0, ps, pe);
+  read_desc(p, 0, 0, ps, pe);
   // Next boundary: this packet's start if it lies inside the region (after a gap),
   // else its end.
   bool start_pending = ps > 0 && ps < kFlatFar;
@@ -1857,11 +1833,17 @@ __global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
   // again: one combine pass serves several groups instead of one pass per boundary.
   uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
   uint32_t pv0 = 0, pv1 = 0, pv2 = 0, pv3 = 0;
-  uint32_t* pdst = nullptr;  // destination of the parked value (null: slot empty)
-  auto flush = [&]() {       // wave-uniform call
+  uint32_t pidx = 0, pkind = 0;  // parked value's packet and kind (0: slot empty, 1: end, 2: start)
+  auto flush = [&]() {           // wave-uniform call
     const uint32_t E = combine_streams_asm(pv0, pv1, pv2, pv3, c.lk);  // lane k == 0
-    if (pdst != nullptr && c.k == 0) *pdst = E;
-    pdst = nullptr;
+    if (pkind != 0u && c.k == 0) (pkind == 2u ? b.e_start : b.e_end)[pidx] = E;
+    pkind = 0;
+  };
+  // Stream bytes at and after a boundary: word j of this lane keeps bytes >= the boundary,
+  // (uint32_t)(~0 << clamp(8 * (x - 4j), 0, 32)) with x the boundary's byte in my chunk.
+  auto above = [](int32_t x8, int32_t j) -> uint32_t {
+    const uint32_t n = (uint32_t)min(max(x8 - 32 * j, 0), 32);
+    return (uint32_t)(~0ull << n);
   };
   for (uint32_t s = 0; s < spg; ++s) {
     const u32x4 v = nextv;
@@ -1876,39 +1858,42 @@ __global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
     h3 = x3;
     const int32_t S0 = 128 * (int32_t)s;
     // Boundaries in (S0, S0 + 128]: park the streams without this step's bytes >= x.
+    // One boundary per group per pass; the state updates are selects (no divergent
+    // branches but the rare window switch).
     while (__builtin_amdgcn_ballot_w64(xn <= S0 + 128)) {
       const bool act = xn <= S0 + 128;
-      if (__builtin_amdgcn_ballot_w64(act && pdst != nullptr)) flush();
-      if (act) {
-        const int32_t B = xn - S0 - c0;
-        pv0 = x0 ^ (v.x & ~bytes_below(B));
-        pv1 = x1 ^ (v.y & ~bytes_below(B - 4));
-        pv2 = x2 ^ (v.z & ~bytes_below(B - 8));
-        pv3 = x3 ^ (v.w & ~bytes_below(B - 12));
-        if (start_pending) {
-          pdst = b.e_start + p;
-          start_pending = false;
-          xn = pe;
-        } else {
-          pdst = b.e_end + p;
-          ++p;
-          if (p - wbase == 8u) {  // window used up: switch windows, refill the other one
-            wbase += 8u;
-            cw ^= 1u;
-            if (s < win_ready) __builtin_amdgcn_s_waitcnt(0);  // the other window's DMA may be in flight
-            if (cw == 1u) dma_desc(std::integral_constant<uint32_t, 0>{}, wbase + 8u);
-            if (cw == 0u) dma_desc(std::integral_constant<uint32_t, 1>{}, wbase + 8u);
-            win_ready = s + (uint32_t)kFlatRing + 1u;
-          }
-          const int32_t prev_end = pe;
-          read_desc(cw, p - wbase, ps, pe);
-          start_pending = ps != prev_end && ps < kFlatFar;
-          xn = start_pending ? ps : pe;
+      if (__builtin_amdgcn_ballot_w64(act && pkind != 0u)) flush();
+      const int32_t x8 = 8 * (xn - S0 - c0);
+      const uint32_t n0 = x0 ^ (v.x & above(x8, 0)), n1 = x1 ^ (v.y & above(x8, 1));
+      const uint32_t n2 = x2 ^ (v.z & above(x8, 2)), n3 = x3 ^ (v.w & above(x8, 3));
+      pv0 = act ? n0 : pv0;
+      pv1 = act ? n1 : pv1;
+      pv2 = act ? n2 : pv2;
+      pv3 = act ? n3 : pv3;
+      pidx = act ? p : pidx;
+      pkind = act ? (start_pending ? 2u : 1u) : pkind;
+      const bool is_end = act && !start_pending;  // a start boundary is followed by its packet's end
+      const uint32_t np = p + (is_end ? 1u : 0u);
+      if (__builtin_amdgcn_ballot_w64(np - wbase == 8u)) {  // a window used up: switch, refill the other
+        if (s < win_ready) __builtin_amdgcn_s_waitcnt(0);    // the other window's DMA may be in flight
+        if (np - wbase == 8u) {
+          wbase += 8u;
+          cw ^= 1u;
+          if (cw == 1u) dma_desc(std::integral_constant<uint32_t, 0>{}, wbase + 8u);
+          if (cw == 0u) dma_desc(std::integral_constant<uint32_t, 1>{}, wbase + 8u);
         }
+        win_ready = s + (uint32_t)kFlatRing + 1u;
       }
+      p = np;
+      int32_t nps, npe;
+      read_desc(p, cw, p - wbase, nps, npe);  // used by the lanes that just passed an end
+      const bool gap = nps != pe && nps < kFlatFar;
+      xn = is_end ? (gap ? nps : npe) : (act ? pe : xn);
+      start_pending = is_end ? gap : (act ? false : start_pending);
+      pe = is_end ? npe : pe;
     }
   }
-  if (__builtin_amdgcn_ballot_w64(pdst != nullptr)) flush();
+  if (__builtin_amdgcn_ballot_w64(pkind != 0u)) flush();
   {
     const uint32_t t = combine_streams_asm(h0, h1, h2, h3, c.lk);  // G_r(R1)
     if (c.k == 0) b.tails[region] = t;
@@ -1916,24 +1901,16 @@ __global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b) {
   __builtin_amdgcn_s_waitcnt(0);  // the ring's last DMAs land before the wave's LDS goes away
 }
 
-// One launch after the main kernel.  Eligible batch: one thread per packet turns the
-// boundary values into checksums.  Otherwise: the streaming kernel's rounds (every
-// packet from scratch; `sb` describes the batch).
-__global__ __launch_bounds__(kBlock) void crc32_flat_finish_kernel(FlatBatch b, Batch<true> sb,
-                                                                   uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
-  if (!flat_batch_ok(b)) {
-    fill_lds(lds);
-    __syncthreads();
-    stream_rounds<kStreamDepth, true>(lds, sb, out);
-    return;
-  }
+// One thread per packet turns the boundary values into checksums (eligible batches; the
+// main kernel ran the fallback rounds otherwise).
+__global__ __launch_bounds__(kBlock) void crc32_flat_finish_kernel(FlatBatch b, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[(kFinFwdLds + kInvLevels) * kSlotLevelDwords + 256 + 64];
+  if (!flat_batch_ok(b)) return;
   // LDS: forward levels 5..5+kFinFwdLds-1, kInvLevels inverse levels, CRC table, inv_top.
   uint32_t* const fwd = lds;
   uint32_t* const inv = lds + kFinFwdLds * kSlotLevelDwords;
   uint32_t* const crc_table = inv + kInvLevels * kSlotLevelDwords;
   uint8_t* const inv_top = reinterpret_cast<uint8_t*>(crc_table + 256);
-  static_assert((kFinFwdLds + kInvLevels) * kSlotLevelDwords + 256 + 64 <= kLdsDwords, "finish LDS");
   const uint32_t* inv_g = b.ladder + kSlotLevels * kSlotLevelDwords;
   const uint32_t* init_tab = inv_g + kInvLevels * kSlotLevelDwords;
   {  // every load issued before the first store (one memory latency, not one per level)
@@ -2226,8 +2203,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     uint64_t ngroups = ((count / 2 + 127) / 128) * 128;
     const uint64_t max_groups = (uint64_t)blocks * kWavesPerBlock * kPacketsPerWave;
     ngroups = ngroups < 128 ? 128 : (ngroups > max_groups ? max_groups : ngroups);
-    constexpr uint64_t kPrepPer = (uint64_t)kFlatPrepBlock * kFlatPrepRun;
-    uint64_t nflags = (count + kPrepPer - 1) / kPrepPer;
+    uint64_t nflags = (count + kFlatPrepBlock - 1) / kFlatPrepBlock;
     nflags = nflags < kFlatMaxFlags ? nflags : kFlatMaxFlags;
     const uint32_t* ladder = nullptr;
     err = device_slot_ladder(&ladder);
@@ -2246,8 +2222,10 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Batch<true> sb = b;
     if (ragged_mode == 4) sb.count = 0;  // ENET_CRC_RAGGED=flatonly: no fallback rounds
     hipLaunchKernelGGL(crc32_flat_prep_kernel, dim3((unsigned)nflags), dim3(kFlatPrepBlock), 0, stream, fb);
-    hipLaunchKernelGGL(crc32_flat_kernel, dim3((unsigned)(ngroups / 128)), dim3(kBlock), 0, stream, fb);
-    hipLaunchKernelGGL(crc32_flat_finish_kernel, dim3(blocks), dim3(kBlock), 0, stream, fb, sb, out);
+    hipLaunchKernelGGL(crc32_flat_kernel, dim3((unsigned)(ngroups / 128)), dim3(kBlock), 0, stream, fb, sb, out);
+    uint64_t fin_blocks = (count + kBlock - 1) / kBlock;
+    fin_blocks = fin_blocks < 2ull * blocks ? fin_blocks : 2ull * blocks;
+    hipLaunchKernelGGL(crc32_flat_finish_kernel, dim3((unsigned)fin_blocks), dim3(kBlock), 0, stream, fb, out);
     err = hipGetLastError();
     const hipError_t ferr = hipFreeAsync(scratch, stream);
     return err != hipSuccess ? err : ferr;
