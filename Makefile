@@ -7,7 +7,7 @@ CC ?= gcc
 LIB := rusty_enet_amd/lib/libenet_crc_amd.so
 ORACLE := oracle/liboracle_crc32.so
 ORACLE_RANGE := oracle/liboracle_range.so
-HIP_SRC := rusty_enet_amd/csrc/crc32_kernels.hip rusty_enet_amd/csrc/crc32_slot.hip rusty_enet_amd/csrc/enet_crc_abi.hip rusty_enet_amd/csrc/range_coder.hip
+HIP_SRC := rusty_enet_amd/csrc/crc32_kernels.hip rusty_enet_amd/csrc/crc32_mailbox.hip rusty_enet_amd/csrc/crc32_slot.hip rusty_enet_amd/csrc/enet_crc_abi.hip rusty_enet_amd/csrc/range_coder.hip
 HIP_DEP := $(HIP_SRC) $(wildcard rusty_enet_amd/csrc/*.hpp) include/enet_crc_amd.h include/enet_range_amd.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -fvisibility=hidden -Wall
 

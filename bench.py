@@ -333,7 +333,8 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
     from rusty_enet_amd import _native
 
     variants = {}
-    for name, mode in (("copy", _native.ENET_CRC_PERCALL_COPY), ("zerocopy", _native.ENET_CRC_PERCALL_ZEROCOPY)):
+    for name, mode in (("copy", _native.ENET_CRC_PERCALL_COPY), ("zerocopy", _native.ENET_CRC_PERCALL_ZEROCOPY),
+                       ("persistent", _native.ENET_CRC_PERCALL_PERSISTENT)):
         ctx.set_percall_mode(mode)
         if ctx.crc32(pkt) != _oracle.crc32(pkt):
             raise SystemExit(f"bench: per-call ({name}) checksum differs from the oracle")
@@ -344,6 +345,7 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
         for _ in range(calls):
             ctx.crc32(pkt)
         variants[name] = round((time.perf_counter() - t0) / calls * 1e6, 2)
+    ctx.set_percall_mode(_native.ENET_CRC_PERCALL_ZEROCOPY)  # stops the server wave
     per_call_us = variants["zerocopy"]  # the context's default mode
     # Floor of any per-call GPU path: one trivial kernel launch + stream synchronize.
     import torch

@@ -31,6 +31,7 @@ pub struct enet_crc_ctx {
 pub const ENET_CRC_OK: c_int = 0;
 pub const ENET_CRC_PERCALL_COPY: c_int = 0;
 pub const ENET_CRC_PERCALL_ZEROCOPY: c_int = 1;
+pub const ENET_CRC_PERCALL_PERSISTENT: c_int = 2;
 
 /// `enet_crc_shard` (include/enet_crc_amd.h): one device-resident batch of a
 /// multi-device launch.  `d_offsets == null` means a uniform shard.
@@ -159,6 +160,17 @@ impl GpuCrc32 {
         }
         let devs: Vec<i32> = (0..n).collect();
         Self::with_devices(&devs)
+    }
+
+    /// How `crc32` moves one datagram: `ENET_CRC_PERCALL_ZEROCOPY` (default),
+    /// `ENET_CRC_PERCALL_COPY`, or `ENET_CRC_PERCALL_PERSISTENT` (a server wave stays on
+    /// the GPU while calls keep coming: no kernel launch per call).
+    pub fn set_percall_mode(&self, mode: i32) -> Result<(), CrcError> {
+        let st = unsafe { enet_crc_ctx_set_percall_mode(self.ctx.0, mode) };
+        if st != ENET_CRC_OK {
+            return Err(last_error(st));
+        }
+        Ok(())
     }
 
     /// Same contract as `rusty_enet::crc32` (src/crc32.rs:39), but fallible.

@@ -114,6 +114,7 @@ class Shard(ctypes.Structure):
 
 ENET_CRC_PERCALL_COPY = 0
 ENET_CRC_PERCALL_ZEROCOPY = 1
+ENET_CRC_PERCALL_PERSISTENT = 2
 
 ABI_VERSION = 3
 

@@ -83,7 +83,8 @@ class Context:
         return lib().enet_crc_ctx_lanes(self._handle)
 
     def set_percall_mode(self, mode: int) -> None:
-        """``_native.ENET_CRC_PERCALL_COPY`` or ``ENET_CRC_PERCALL_ZEROCOPY`` (default)."""
+        """``_native.ENET_CRC_PERCALL_COPY``, ``ENET_CRC_PERCALL_ZEROCOPY`` (default) or
+        ``ENET_CRC_PERCALL_PERSISTENT`` (a resident server wave; include/enet_crc_amd.h)."""
         check(lib().enet_crc_ctx_set_percall_mode(self._handle, mode), "enet_crc_ctx_set_percall_mode")
 
     @property

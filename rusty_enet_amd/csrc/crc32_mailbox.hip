@@ -1,0 +1,147 @@
+// Persistent per-call checksum server (crc32_mailbox.hpp).
+//
+// A request is the datagram's bytes right-aligned in a 4096-B window: 64 chunks of
+// 64 B, one per lane; chunks wholly below the datagram are zero and skipped (zero bytes
+// in front do not change a zero-initialised register).  Each lane runs its chunk's 16
+// words through four interleaved M32^4 streams and one M32 Horner (4 LDS lookups per
+// step), then a 6-level
+// shuffle tree joins the 64 chunk registers: level k moves the left half of each pair
+// over 64 * 2^k bytes, M32^(16 * 2^k) (ladder level 4 + k).  Lane 0 returns the
+// register of the window; the host adds M8^len(0xFFFFFFFF) and finishes bswap32(~reg)
+// (src/crc32.rs:39-47).
+//
+// Every access to the mailbox is a vector load or store with system scope (sc0 sc1) in
+// inline asm, so nothing is cached between polls and each store has reached host memory
+// before the next one is issued (s_waitcnt vmcnt(0)).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32_mailbox.hpp"
+#include "crc32_slot.hpp"
+
+namespace enet_crc {
+namespace {
+
+typedef uint32_t u32x4m __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  uint32_t v;
+  asm volatile(
+      "global_load_dword %0, %1, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=v"(v)
+      : "v"(p)
+      : "memory");
+  return v;
+}
+
+// 64 bytes at p (16-B aligned): four loads in flight, one wait.
+__device__ __forceinline__ void sys_load64(const uint8_t* p, u32x4m& a, u32x4m& b, u32x4m& c, u32x4m& d) {
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off sc0 sc1\n\t"
+      "global_load_dwordx4 %1, %4, off offset:16 sc0 sc1\n\t"
+      "global_load_dwordx4 %2, %4, off offset:32 sc0 sc1\n\t"
+      "global_load_dwordx4 %3, %4, off offset:48 sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+      : "v"(p)
+      : "memory");
+}
+
+// Two adjacent words in one load (the host writes them with one 64-bit store).
+__device__ __forceinline__ void sys_load2(const uint32_t* p, uint32_t& lo, uint32_t& hi) {
+  uint64_t v;
+  asm volatile(
+      "global_load_dwordx2 %0, %1, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=v"(v)
+      : "v"(p)
+      : "memory");
+  lo = (uint32_t)v;
+  hi = (uint32_t)(v >> 32);
+}
+
+// Two adjacent words in one store (the host reads them with one 64-bit load).
+__device__ __forceinline__ void sys_store2(uint32_t* p, uint32_t lo, uint32_t hi) {
+  const uint64_t v = ((uint64_t)hi << 32) | lo;
+  asm volatile(
+      "global_store_dwordx2 %0, %1, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      :
+      : "v"(p), "v"(v)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t apply4(const uint32_t* t, uint32_t x) {
+  return t[x & 0xffu] ^ t[256 + ((x >> 8) & 0xffu)] ^ t[512 + ((x >> 16) & 0xffu)] ^ t[768 + (x >> 24)];
+}
+
+constexpr int kMbLevels = 6;  // 64 chunks
+
+__global__ __launch_bounds__(64) void crc32_mailbox_kernel(Mailbox* mb, const uint32_t* __restrict__ ladder) {
+  __shared__ uint32_t m32[kSlotLevelDwords];               // ladder level 0: M32
+  __shared__ uint32_t m32x4[kSlotLevelDwords];             // ladder level 2: M32^4
+  __shared__ uint32_t lv[kMbLevels][kSlotLevelDwords];     // ladder levels 4 .. 9
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t x = lane; x < kSlotLevelDwords; x += 64) {
+    m32[x] = ladder[x];
+    m32x4[x] = ladder[2 * kSlotLevelDwords + x];
+#pragma unroll
+    for (int k = 0; k < kMbLevels; ++k) lv[k][x] = ladder[(4 + k) * kSlotLevelDwords + x];
+  }
+  __syncthreads();
+  uint32_t last = __builtin_amdgcn_readfirstlane(sys_load(&mb->done));
+  const uint64_t t0 = wall_clock64();
+  uint64_t t_last = t0;
+  for (;;) {
+    uint32_t seq, len;
+    sys_load2(&mb->seq, seq, len);  // one 64-bit word: the host posts both with one store
+    seq = __builtin_amdgcn_readfirstlane(seq);
+    len = __builtin_amdgcn_readfirstlane(len);
+    if (seq == kMailboxStop) break;
+    const uint64_t now = wall_clock64();
+    if (seq == last) {
+      if (now - t_last > kMailboxIdleTicks || now - t0 > kMailboxMaxTicks) break;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    const uint32_t first_chunk = (kMailboxBytes - (len < kMailboxBytes ? len : kMailboxBytes)) / 64u;
+    uint32_t r = 0;
+    if (lane >= first_chunk) {
+      const uint8_t* src = mb->data + 64u * lane;
+      u32x4m v[4];
+      sys_load64(src, v[0], v[1], v[2], v[3]);
+      // Four interleaved word streams (word 4i + j in stream j, steps of M32^4), then
+      // one M32 Horner over the four: 4 + 3 dependent lookup rounds instead of 16.
+      uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a0 = apply4(m32x4, a0) ^ v[i].x;
+        a1 = apply4(m32x4, a1) ^ v[i].y;
+        a2 = apply4(m32x4, a2) ^ v[i].z;
+        a3 = apply4(m32x4, a3) ^ v[i].w;
+      }
+      r = apply4(m32, a0) ^ a1;
+      r = apply4(m32, r) ^ a2;
+      r = apply4(m32, r) ^ a3;
+      r = apply4(m32, r);  // the last word's own step: reg = M32(reg ^ w)
+    }
+#pragma unroll
+    for (int k = 0; k < kMbLevels; ++k) {
+      const uint32_t right = (uint32_t)__shfl_down((int)r, 1 << k, 64);
+      if ((lane & ((2u << k) - 1u)) == 0) r = apply4(lv[k], r) ^ right;
+    }
+    if (lane == 0) sys_store2(&mb->done, seq, r);  // done and result in one 64-bit store
+    last = seq;
+    t_last = now;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_mailbox(Mailbox* mb, const uint32_t* ladder, hipStream_t stream) {
+  hipLaunchKernelGGL(crc32_mailbox_kernel, dim3(1), dim3(64), 0, stream, mb, ladder);
+  return hipGetLastError();
+}
+
+}  // namespace enet_crc

@@ -1,0 +1,36 @@
+// Persistent per-call checksum server (ENET_CRC_PERCALL_PERSISTENT, enet_crc32_iov):
+// one wave polls a mailbox in pinned, coherent host memory, checksums each datagram
+// the host posts there and writes the register back, so a call costs PCIe round trips
+// instead of a kernel launch plus a stream synchronisation.  Shared by
+// crc32_mailbox.hip (the kernel) and enet_crc_abi.hip (the host side).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace enet_crc {
+
+constexpr uint32_t kMailboxBytes = 4096;         // largest datagram served (PROTOCOL_MAXIMUM_MTU)
+constexpr uint32_t kMailboxStop = 0xFFFFFFFFu;   // seq value that makes the server exit
+constexpr uint64_t kMailboxIdleTicks = 2000000;  // 20 ms of the 100-MHz wall clock without a request: exit
+constexpr uint64_t kMailboxMaxTicks = 200000000; // 2 s: exit (the host relaunches on the next call)
+
+// Host and device view of the mailbox; the three groups of fields sit on separate lines.
+// seq/len and done/result are each written with one 64-bit store and read with one
+// 64-bit load (one PCIe round trip each).
+struct alignas(128) Mailbox {
+  uint32_t seq;  // host -> server: number of the posted request (kMailboxStop: exit)
+  uint32_t len;  // bytes of the posted request, right-aligned at the end of data
+  uint32_t pad0[30];
+  uint32_t done;    // server -> host: number of the last request served
+  uint32_t result;  // its zero-initialised register (the initial register is added on the host)
+  uint32_t pad1[30];
+  uint8_t data[kMailboxBytes];  // request bytes end at data + kMailboxBytes; the 64-B chunk
+                                // holding the first byte is zero below it
+};
+
+// Starts the server wave on `stream` (`mb` is the device address of the mailbox,
+// `ladder` the device ladder of crc32_slot.hpp).  The kernel returns on kMailboxStop,
+// after kMailboxIdleTicks without a request, or after kMailboxMaxTicks.
+hipError_t launch_mailbox(Mailbox* mb, const uint32_t* ladder, hipStream_t stream);
+
+}  // namespace enet_crc

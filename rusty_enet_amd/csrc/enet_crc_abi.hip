@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -29,6 +30,7 @@
 #include "../../include/enet_crc_amd.h"
 #include "../../include/enet_range_amd.h"
 #include "crc32_kernels.hpp"
+#include "crc32_mailbox.hpp"
 #include "crc32_slot.hpp"
 #include "range_coder.hpp"
 
@@ -230,11 +232,17 @@ struct RangeStage {
 };
 
 // Per-call (enet_crc32_iov) buffers: a pinned, device-mapped input buffer the kernel
-// reads directly (zero-copy mode) and a mapped result word.
+// reads directly (zero-copy mode), a mapped result word, and the persistent server's
+// mailbox (pinned, coherent, mapped) with its stream.
 struct PerCall {
   uint8_t* h_in = nullptr;
   size_t cap = 0;
   uint32_t* h_res = nullptr;  // [0] = checksum (mapped: written by the kernel)
+  Mailbox* mb = nullptr;      // host address of the mailbox
+  Mailbox* d_mb = nullptr;    // its device address
+  hipStream_t mb_stream = nullptr;
+  bool mb_launched = false;   // a server was launched and may still run
+  uint32_t mb_seq = 0;        // last request number posted
 };
 
 // A worker thread bound to one lane: runs one job at a time for the calling thread.
@@ -521,20 +529,44 @@ int enet_crc_ctx_create(int device, enet_crc_ctx** out_ctx) { return enet_crc_ct
 
 int enet_crc_ctx_lanes(const enet_crc_ctx* ctx) { return ctx ? (int)ctx->lanes.size() : ENET_CRC_E_INVALID; }
 
+namespace {
+
+// Ask a running server to exit and wait until it has (its stream drains).
+void stop_mailbox(PerCall& c) {
+  if (!c.mb_launched) return;
+  __atomic_store_n(&c.mb->seq, kMailboxStop, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(c.mb_stream);
+  c.mb_launched = false;
+}
+
+}  // namespace
+
 int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode) {
-  if (!ctx || (mode != ENET_CRC_PERCALL_COPY && mode != ENET_CRC_PERCALL_ZEROCOPY)) return ENET_CRC_E_INVALID;
+  if (!ctx || (mode != ENET_CRC_PERCALL_COPY && mode != ENET_CRC_PERCALL_ZEROCOPY &&
+               mode != ENET_CRC_PERCALL_PERSISTENT))
+    return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
+  if (mode != ENET_CRC_PERCALL_PERSISTENT && ctx->call.mb_launched) {
+    DeviceGuard g(ctx->lanes[0].device);
+    stop_mailbox(ctx->call);
+  }
   ctx->percall_mode = mode;
   return ENET_CRC_OK;
 }
 
 void enet_crc_ctx_destroy(enet_crc_ctx* ctx) {
   if (!ctx) return;
+  if (!ctx->lanes.empty()) {
+    DeviceGuard g(ctx->lanes[0].device);
+    stop_mailbox(ctx->call);
+  }
   for (auto& L : ctx->lanes) destroy_lane(L);
   if (!ctx->lanes.empty()) {
     DeviceGuard g(ctx->lanes[0].device);
     if (ctx->call.h_in) (void)hipHostFree(ctx->call.h_in);
     if (ctx->call.h_res) (void)hipHostFree(ctx->call.h_res);
+    if (ctx->call.mb) (void)hipHostFree(ctx->call.mb);
+    if (ctx->call.mb_stream) (void)hipStreamDestroy(ctx->call.mb_stream);
   }
   delete ctx;
 }
@@ -630,7 +662,52 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
   DeviceGuard g(L.device);
   StageSlot& s = L.slot[0];
   quiesce(L);  // nothing of an earlier (failed) call may still use the buffers
-  if (ctx->percall_mode == ENET_CRC_PERCALL_ZEROCOPY) {
+  if (ctx->percall_mode == ENET_CRC_PERCALL_PERSISTENT && total <= kMailboxBytes) {
+    // Post the datagram to the server wave's mailbox and spin on its answer; launch the
+    // server when none runs (first call, or it exited after kMailboxIdleTicks idle).
+    PerCall& c = ctx->call;
+    if (!c.mb) {
+      ENET_HIP_TRY(hipHostMalloc((void**)&c.mb, sizeof(Mailbox), hipHostMallocMapped | hipHostMallocCoherent));
+      memset(c.mb, 0, sizeof(Mailbox));
+      ENET_HIP_TRY(hipHostGetDevicePointer((void**)&c.d_mb, c.mb, 0));
+      ENET_HIP_TRY(hipStreamCreateWithFlags(&c.mb_stream, hipStreamNonBlocking));
+    }
+    const uint32_t* ladder = nullptr;
+    ENET_HIP_TRY(device_slot_ladder(&ladder));
+    uint8_t* dst = c.mb->data + (kMailboxBytes - total);  // right-aligned; zero below it in its chunk
+    memset(c.mb->data + ((kMailboxBytes - total) & ~(size_t)63), 0, (kMailboxBytes - total) & 63);
+    size_t pos = 0;  // concatenation, src/crc32.rs:41-42
+    for (size_t i = 0; i < nbufs; ++i) {
+      if (bufs[i].len) memcpy(dst + pos, bufs[i].data, bufs[i].len);
+      pos += bufs[i].len;
+    }
+    c.mb_seq = c.mb_seq + 1 == kMailboxStop ? 1u : c.mb_seq + 1;
+    const uint32_t seq = c.mb_seq;
+    // seq and len in one 64-bit store, ordered after the bytes.
+    __atomic_store_n(reinterpret_cast<uint64_t*>(&c.mb->seq), ((uint64_t)total << 32) | seq, __ATOMIC_RELEASE);
+    auto launch = [&]() -> hipError_t {
+      const hipError_t e = launch_mailbox(c.d_mb, ladder, c.mb_stream);
+      c.mb_launched = e == hipSuccess;
+      return e;
+    };
+    if (!c.mb_launched || hipStreamQuery(c.mb_stream) == hipSuccess) ENET_HIP_TRY(launch());
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t* answer = reinterpret_cast<const uint64_t*>(&c.mb->done);  // done | result << 32
+    uint64_t a = 0;
+    for (uint32_t n = 1; (uint32_t)(a = __atomic_load_n(answer, __ATOMIC_ACQUIRE)) != seq; ++n) {
+      if ((n & 1023u) == 0) {
+        // The server may have exited (idle limit) just before this request: relaunch.
+        if (hipStreamQuery(c.mb_stream) == hipSuccess && (uint32_t)__atomic_load_n(answer, __ATOMIC_ACQUIRE) != seq)
+          ENET_HIP_TRY(launch());
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return fail_hip(hipErrorLaunchTimeOut);
+      }
+      __builtin_ia32_pause();
+    }
+    const uint32_t reg = (uint32_t)(a >> 32) ^ host_slot_ladder()[kLadderLevels * kSlotLevelDwords + total];
+    *out_crc = __builtin_bswap32(~reg);
+    return ENET_CRC_OK;
+  }
+  if (ctx->percall_mode != ENET_CRC_PERCALL_COPY) {
     // The kernel reads the gathered bytes straight from pinned host memory and writes
     // the checksum into mapped host memory: no copy engine on the path.
     PerCall& c = ctx->call;

@@ -102,7 +102,8 @@ def test_shards_device_two_shards(dev):
     assert np.array_equal(ob.cpu().numpy().view(np.uint32), _oracle.crc32_ragged(b, offsets, lengths))
 
 
-@pytest.mark.parametrize("mode", [_native.ENET_CRC_PERCALL_COPY, _native.ENET_CRC_PERCALL_ZEROCOPY])
+@pytest.mark.parametrize("mode", [_native.ENET_CRC_PERCALL_COPY, _native.ENET_CRC_PERCALL_ZEROCOPY,
+                                  _native.ENET_CRC_PERCALL_PERSISTENT])
 def test_per_call_modes(dev, mode):
     with rea.Context(0) as ctx:
         ctx.set_percall_mode(mode)
@@ -116,6 +117,30 @@ def test_per_call_modes(dev, mode):
         for trial in range(10):
             slices = [splitmix64_bytes(100 * trial + j, int(rng.integers(0, 40)) if j < 9 else 0) for j in range(65)]
             assert ctx(slices) == _oracle.crc32(slices)
+
+
+def test_persistent_server_lifecycle(dev):
+    """ENET_CRC_PERCALL_PERSISTENT: every length a datagram can have (0..4096, the
+    mailbox window) bit-exact, across the server's idle exit and relaunch, a switch to
+    another mode and back, and destroying the context while the server runs."""
+    import time
+    rng = np.random.default_rng(11)
+    with rea.Context(0) as ctx:
+        ctx.set_percall_mode(_native.ENET_CRC_PERCALL_PERSISTENT)
+        for n in list(range(0, 130)) + [int(x) for x in rng.integers(130, 4097, 300)] + [4096]:
+            buf = splitmix64_bytes(7 * n + 1, n)
+            cut = int(rng.integers(0, n + 1))
+            assert ctx([buf[:cut], buf[cut:]]) == _oracle.crc32([buf]), n
+        time.sleep(0.1)  # > 20 ms idle: the server has exited; the next call relaunches it
+        assert ctx([bytes([1, 2, 3, 4, 5, 6, 7, 8])]) == 3314076223
+        ctx.set_percall_mode(_native.ENET_CRC_PERCALL_ZEROCOPY)  # stops the server
+        assert ctx([b"abc"]) == _oracle.crc32([b"abc"])
+        ctx.set_percall_mode(_native.ENET_CRC_PERCALL_PERSISTENT)
+        assert ctx([b"abc"]) == _oracle.crc32([b"abc"])
+    # the context was destroyed with the server running; a new one starts its own
+    with rea.Context(0) as ctx:
+        ctx.set_percall_mode(_native.ENET_CRC_PERCALL_PERSISTENT)
+        assert ctx([b"123456789"]) == _oracle.crc32([b"123456789"])
 
 
 def test_stream_device_is_used(dev):
