@@ -346,7 +346,7 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
             ctx.crc32(pkt)
         variants[name] = round((time.perf_counter() - t0) / calls * 1e6, 2)
     ctx.set_percall_mode(_native.ENET_CRC_PERCALL_ZEROCOPY)  # stops the server wave
-    per_call_us = variants["zerocopy"]  # the context's default mode
+    per_call_us = variants["persistent"]  # the context's default mode
     # Floor of any per-call GPU path: one trivial kernel launch + stream synchronize.
     import torch
 
@@ -371,7 +371,8 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
             "per_call_variants_us": variants,
             "per_call_cpu_oracle_us": round(cpu_call_us, 2),
             "per_call_floor_us": round(floor_us, 2),
-            "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000; "
+            "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000, "
+                               "default mode (persistent server wave; variants: copy, zero-copy launch, persistent); "
                                "cpu: the C restatement of src/crc32.rs on the same datagram through ctypes; floor: one "
                                "trivial torch kernel launch + torch.cuda.synchronize",
             "ring": ring_rate(dev, L)}

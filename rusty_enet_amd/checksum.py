@@ -15,6 +15,7 @@ for; the per-call path pays a launch + two PCIe copies per datagram.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import threading
 from typing import Iterable, Optional, Sequence
@@ -83,8 +84,8 @@ class Context:
         return lib().enet_crc_ctx_lanes(self._handle)
 
     def set_percall_mode(self, mode: int) -> None:
-        """``_native.ENET_CRC_PERCALL_COPY``, ``ENET_CRC_PERCALL_ZEROCOPY`` (default) or
-        ``ENET_CRC_PERCALL_PERSISTENT`` (a resident server wave; include/enet_crc_amd.h)."""
+        """``_native.ENET_CRC_PERCALL_COPY``, ``ENET_CRC_PERCALL_ZEROCOPY`` or
+        ``ENET_CRC_PERCALL_PERSISTENT`` (default: a resident server wave; include/enet_crc_amd.h)."""
         check(lib().enet_crc_ctx_set_percall_mode(self._handle, mode), "enet_crc_ctx_set_percall_mode")
 
     @property
@@ -191,9 +192,20 @@ def default_context(device: int = 0) -> Context:
     with _default_lock:
         ctx = _default.get(device)
         if ctx is None:
+            if not _default:
+                atexit.register(_close_defaults)
             ctx = Context(device)
             _default[device] = ctx
         return ctx
+
+
+def _close_defaults() -> None:
+    """At interpreter exit: stop each default context's per-call server wave (it would
+    otherwise run until its 20-ms idle limit while the process tears the device down)."""
+    with _default_lock:
+        for ctx in _default.values():
+            ctx.close()
+        _default.clear()
 
 
 def crc32(in_buffers: Sequence) -> int:

@@ -309,7 +309,7 @@ struct enet_crc_ctx {
   std::mutex lock;
   std::vector<Lane> lanes;
   PerCall call;
-  int percall_mode = ENET_CRC_PERCALL_ZEROCOPY;
+  int percall_mode = ENET_CRC_PERCALL_PERSISTENT;
 };
 
 // One slot of a pinned receive ring (include/enet_crc_amd.h).
@@ -541,6 +541,14 @@ void stop_mailbox(PerCall& c) {
 
 }  // namespace
 
+// Batch entry points of a context stop its server wave first: a resident wave holds
+// one CU, and the batched kernels size their grids to every CU.
+static void stop_server_for_batch(enet_crc_ctx* ctx) {
+  if (!ctx->call.mb_launched) return;
+  DeviceGuard g(ctx->lanes[0].device);
+  stop_mailbox(ctx->call);
+}
+
 int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode) {
   if (!ctx || (mode != ENET_CRC_PERCALL_COPY && mode != ENET_CRC_PERCALL_ZEROCOPY &&
                mode != ENET_CRC_PERCALL_PERSISTENT))
@@ -757,6 +765,7 @@ int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t
   if (count == 0) return ENET_CRC_OK;
   if (!h_base || !h_offsets || !h_lengths || !h_out) return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
+  stop_server_for_batch(ctx);
   const uint8_t* base = static_cast<const uint8_t*>(h_base);
   const uint32_t nl = (uint32_t)std::min<uint64_t>(ctx->lanes.size(), count);
   if (nl <= 1) return ragged_host_shard(ctx->lanes[0], base, h_offsets, h_lengths, count, h_out);
@@ -1069,6 +1078,7 @@ static int range_ragged_host(enet_crc_ctx* ctx, bool decompress, const void* h_i
   if (!h_in || !h_in_offsets || !h_in_lengths || !h_out || !h_out_offsets || !h_out_limits || !h_sizes)
     return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
+  stop_server_for_batch(ctx);
   return range_host(ctx, decompress, static_cast<const uint8_t*>(h_in), h_in_offsets, h_in_lengths, count,
                     static_cast<uint8_t*>(h_out), h_out_offsets, h_out_limits, h_sizes);
 }
