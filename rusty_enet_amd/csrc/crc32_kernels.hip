@@ -656,6 +656,7 @@ struct UniformBatch {
   uint64_t stride;
   uint32_t length;
   uint64_t count;
+  uint32_t xcd_swizzle = 1;  // ENET_CRC_XCD=0 turns the XCD-aware round order off (A/B runs)
 };
 
 // ---------------------------------------------------------------------------------
@@ -759,6 +760,17 @@ __device__ __forceinline__ void horner_step_and_read(const Lookup& lk, uint32_t&
       : "memory");
 }
 
+// Logical block index under which the workgroups sharing an XCD (blockIdx % 8, as the
+// dispatcher is observed to place them) get consecutive indices, i.e. neighbouring
+// packets: the 128-B line two packets of adjacent rounds share is then fetched into one
+// XCD's L2 instead of two (bijective for any grid: cdna_hip_programming.md §5.5 T1).
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t orig, uint32_t nwg) {
+  constexpr uint32_t kXcds = 8;
+  if (nwg <= kXcds) return orig;
+  const uint32_t q = nwg / kXcds, r = nwg % kXcds, xcd = orig % kXcds;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / kXcds;
+}
+
 // LDS atomic add in asm: hipcc would otherwise order it behind every in-flight LDS-DMA
 // (it cannot tell the counter from the ring) and drain the ring with vmcnt(0).
 __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
@@ -805,8 +817,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
 
   const uint64_t total_rounds = (u.count + kPacketsPerWave - 1) / kPacketsPerWave;
   const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t lb = u.xcd_swizzle ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
   auto round_of = [&](uint32_t d) -> uint64_t {
-    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+    return (uint64_t)lb * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
   };
 
   const uint32_t lx = (u.length + 3u) & ~3u, z = lx - u.length;
@@ -2100,7 +2113,9 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
     const int nsx = make_geo(0, (length + 3u) & ~3u).nsteps;
     const unsigned blocks = grid_for(count, err);
     if (err != hipSuccess) return err;
-    const UniformBatch u{b0, stride, length, count};
+    UniformBatch u{b0, stride, length, count};
+    const char* xv = getenv("ENET_CRC_XCD");
+    u.xcd_swizzle = (xv && strcmp(xv, "0") == 0) ? 0u : 1u;
     if (use_regs_uniform() && nsx <= kMaxRoundSteps)
       return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
     return dispatch_uniform_dma(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
