@@ -440,11 +440,12 @@ def load_pmc_traffic(config: str):
 
 
 def range_roofline(nbytes: int, kernel_ms: float, kernel_ms_max: float) -> dict:
-    """The range coder is bound by dependent arena accesses (each 16-B node read is its own
-    memory transaction), not by streaming bandwidth.  With the HBM read requests per
-    launch from the committed profile (TCC_EA0_RDREQ, same kernel sources), the achieved
-    rate is expressed as 64-B read requests per second against the HBM's 8 TB/s / 64 B
-    = 125 G requests/s; without it, only the input rate is reported."""
+    """The range coder is bound by dependent arena accesses (each 16-B node
+    read-modify-write is its own memory transaction), not by streaming bandwidth.  With
+    the HBM read + write requests per launch from the committed profile (TCC_EA0_RDREQ,
+    TCC_EA0_WRREQ; same kernel sources), the achieved rate is expressed as 64-B requests
+    per second against the HBM's 8 TB/s / 64 B = 125 G requests/s; without it, only the
+    input rate is reported."""
     achieved_in = nbytes / (kernel_ms / 1000.0) / 1e9
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     req = None
@@ -453,6 +454,8 @@ def range_roofline(nbytes: int, kernel_ms: float, kernel_ms_max: float) -> dict:
             v = json.load(f).get("range")
         if v and v.get("source_hash") == kernel_source_hash():
             req = v.get("read_requests_per_launch")
+            if req and v.get("write_requests_per_launch"):
+                req += v["write_requests_per_launch"]
     except (OSError, ValueError):
         pass
     out = {"bound": "latency", "input_gbs": round(achieved_in, 3), "kernel_ms": round(kernel_ms, 3),

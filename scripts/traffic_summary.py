@@ -42,19 +42,23 @@ for cfg in ("uniform", "ragged", "large"):
     main = max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
     out[cfg] = {"kernel": main, "hbm_bytes_per_launch": kernels[main]["hbm_bytes_per_launch"],
                 "kernels": kernels, "source": os.path.relpath(root), "source_hash": src_hash}
-# Range coder (compress kernel): memory-side read requests per launch (random 16-B node
-# accesses, each its own request; bench.py range_roofline turns them into a request rate).
-req, dur = [], None
+# Range coder (compress kernel): memory-side read and write requests per launch (random
+# 16-B node read-modify-writes, each its own request; bench.py range_roofline turns them
+# into a request rate).
+req, wreq, dur = [], [], None
 for path in glob.glob(os.path.join(root, "pmc_range", "**", "*counter_collection*.csv"), recursive=True):
     for r in csv.DictReader(open(path)):
         if "range_coder_kernel<false>" in r["Kernel_Name"] and r["Counter_Name"].startswith("TCC_EA0_RDREQ"):
             req.append(float(r["Counter_Value"]))
+        if "range_coder_kernel<false>" in r["Kernel_Name"] and r["Counter_Name"].startswith("TCC_EA0_WRREQ"):
+            wreq.append(float(r["Counter_Value"]))
 for path in glob.glob(os.path.join(root, "prof_range", "**", "*kernel_stats*.csv"), recursive=True):
     for r in csv.DictReader(open(path)):
         if "range_coder_kernel<false>" in r["Name"]:
             dur = float(r["AverageNs"])
 if req:
     out["range"] = {"kernel": "range_coder_kernel<false>", "read_requests_per_launch": sum(req) / len(req),
+                    "write_requests_per_launch": sum(wreq) / len(wreq) if wreq else None,
                     "launches": len(req), "mean_duration_ns": dur, "source": os.path.relpath(root),
                     "source_hash": src_hash}
 print(json.dumps(out, indent=1))
