@@ -107,7 +107,7 @@ def spawn(args, argv: list[str]) -> int:
 # workloads
 # --------------------------------------------------------------------------------------
 
-def make_workload(name: str, rank: int, n: int, dev):
+def make_workload(name: str, rank: int, n: int, dev, length: int | None = None):
     import torch
 
     import rusty_enet_amd as rea
@@ -116,7 +116,7 @@ def make_workload(name: str, rank: int, n: int, dev):
     g = torch.Generator(device=dev)
     g.manual_seed(ENET_SEED + 7919 * rank)
     if name in ("uniform", "large"):
-        L = 1200 if name == "uniform" else 65536
+        L = length or (1200 if name == "uniform" else 65536)
         data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         step = lambda: rea.crc32_batch(data, stride=L, length=L, count=n, out=out)  # noqa: E731
@@ -490,10 +490,14 @@ def time_steps(step, steps: int, barrier, dev) -> tuple[float, float]:
 
 def shard_2m(dev, rank: int, steps: int, warmup: int, barrier) -> dict:
     """The N > 1 per-GPU shard (2M x 1200 B) timed on this GPU, at N = 1."""
+    return uniform_point(dev, rank, CONFIGS["uniform"][2], 1200, steps, warmup, barrier)
+
+
+def uniform_point(dev, rank: int, n: int, L: int, steps: int, warmup: int, barrier) -> dict:
+    """n x L-byte uniform packets timed on this GPU (verified on a sample first)."""
     import torch
 
-    n = CONFIGS["uniform"][2]
-    step, nbytes, _, out, spec = make_workload("uniform", rank, n, dev)
+    step, nbytes, _, out, spec = make_workload("uniform", rank, n, dev, length=L)
     step()
     torch.cuda.synchronize()
     verify_sample(out, spec)
@@ -578,6 +582,9 @@ def main(argv=None) -> int:
         del step, out, spec
         torch.cuda.empty_cache()
         extra["shard_2m"] = shard_2m(dev, rank, min(args.steps, 100), args.warmup, barrier)
+        # The reference's default MTU (src/consts.rs:32; SURVEY.md 8(a) note): 1M x 1392 B.
+        extra["mtu_1392"] = uniform_point(dev, rank, CONFIGS["uniform"][1], 1392, min(args.steps, 100), args.warmup,
+                                          barrier)
 
     if rank == 0:
         total_bytes = nbytes * world
