@@ -656,7 +656,7 @@ struct UniformBatch {
   uint64_t stride;
   uint32_t length;
   uint64_t count;
-  uint32_t xcd_swizzle = 1;  // ENET_CRC_XCD=0 turns the XCD-aware round order off (A/B runs)
+  uint32_t xcd_swizzle = 0;  // ENET_CRC_XCD=1: XCD-aware round order (A/B runs; off: DESIGN.md §6)
 };
 
 // ---------------------------------------------------------------------------------
@@ -2115,7 +2115,7 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
     if (err != hipSuccess) return err;
     UniformBatch u{b0, stride, length, count};
     const char* xv = getenv("ENET_CRC_XCD");
-    u.xcd_swizzle = (xv && strcmp(xv, "0") == 0) ? 0u : 1u;
+    u.xcd_swizzle = (xv && strcmp(xv, "1") == 0) ? 1u : 0u;
     if (use_regs_uniform() && nsx <= kMaxRoundSteps)
       return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
     return dispatch_uniform_dma(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
