@@ -2093,14 +2093,13 @@ static hipError_t dispatch_uniform_regs(int ns, const UniformBatch& u, uint32_t*
   return e;
 }
 
-// Aligned uniform batches run the LDS-DMA kernel; ENET_CRC_UNIFORM=regs selects the
-// register-ring kernel instead (packets of up to kMaxRoundSteps steps; A/B runs).
+// Aligned uniform batches of packets up to kMaxRoundSteps steps (≤ 1792 B) run the
+// register-ring kernel, longer ones the LDS-DMA kernel.  Every alternating A/B so far
+// had the register ring 1-3 % ahead on G1; ENET_CRC_UNIFORM=dma selects
+// the LDS-DMA kernel for all lengths (A/B runs).  Read per launch.
 static bool use_regs_uniform() {
-  static const bool regs = [] {
-    const char* v = getenv("ENET_CRC_UNIFORM");
-    return v && strcmp(v, "regs") == 0;
-  }();
-  return regs;
+  const char* v = getenv("ENET_CRC_UNIFORM");
+  return !(v && strcmp(v, "dma") == 0);
 }
 
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
