@@ -649,6 +649,122 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_records_kernel(Batch<t
   }
 }
 
+// Region records (the default pre-pass): the batch in regions of R consecutive packets,
+// each sorted by step class on its own, stably (address order within a class), into the
+// region's own range of round records.  One workgroup per region, one launch, no global
+// histogram.  Rounds that straddle a class boundary inside a region (at most 15 per
+// region) run the ragged kernel's generic path.  With R = 16 x the ragged kernel's grid,
+// region k = 8 s + x is exactly the set of rounds the workgroups of XCD x take in sweep s
+// (RaggedDmaBatch::xcd_rounds), so the 128-B line two neighbouring packets share is read
+// by the same L2 within one sweep instead of twice from HBM (the global sort separates
+// such neighbours by up to the whole launch).
+constexpr int kRegionPer = 4;                           // packets per thread (consecutive)
+constexpr int kRegionBlock = 1024;
+constexpr int kRegionWaves = kRegionBlock / 64;
+constexpr uint32_t kRegionMax = kRegionPer * kRegionBlock;  // 4096 packets, 64 KiB of records
+
+// Inclusive prefix sum over the 64 lanes in DPP (no LDS round trips): shifts of 1, 2, 4
+// and 8 inside each 16-lane row, then row 0's and row 1's last lanes broadcast into the
+// rows above (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).
+__device__ __forceinline__ uint32_t wave_inclusive_add(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
+__global__ __launch_bounds__(kRegionBlock) void crc32_region_records_kernel(Batch<true> b, uint32_t region,
+                                                                             uint8_t* __restrict__ recs) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kRegionMax / kPacketsPerWave * kRecordBytes];
+  __shared__ uint32_t wtot[kRegionWaves][8], wpre[kRegionWaves + 1][8];
+  const uint64_t lo = (uint64_t)blockIdx.x * region;
+  const uint32_t n = (uint32_t)(b.count - lo < region ? b.count - lo : region);
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t first = t * kRegionPer;
+  uint64_t sa[kRegionPer];
+  uint32_t len[kRegionPer];
+#pragma unroll
+  for (int k = 0; k < kRegionPer; ++k) {
+    const bool v = first + k < n;
+    sa[k] = v ? b.offsets[lo + first + k] : 0;
+    len[k] = v ? b.lengths[lo + first + k] : 0;
+  }
+  // Class per packet (kStepClasses for the lanes past the region end), each packet's rank
+  // among this thread's packets of its class, and the thread's class counts as 16-bit
+  // fields (class c: word c/2, half c%2).  Static indices only: a dynamically indexed
+  // register array goes to scratch.
+  uint32_t cls[kRegionPer], rank[kRegionPer], cnt[8];
+#pragma unroll
+  for (int k = 0; k < kRegionPer; ++k) {
+    sa[k] += b.base;
+    cls[k] = first + k < n ? step_class_of(sa[k], len[k]) : (uint32_t)kStepClasses;
+    rank[k] = 0;
+#pragma unroll
+    for (int j = 0; j < k; ++j) rank[k] += cls[j] == cls[k] ? 1u : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) {
+    cnt[i] = 0;
+#pragma unroll
+    for (int k = 0; k < kRegionPer; ++k) cnt[i] += (cls[k] >> 1) == i ? 1u << (16u * (cls[k] & 1u)) : 0u;
+  }
+  // Exclusive prefix over the threads of the block (fields never carry: sums <= 4096):
+  // inclusive scan per wave, then the 16 wave totals scanned by 128 threads.
+  uint32_t inc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) inc[i] = cnt[i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) inc[i] = wave_inclusive_add(inc[i]);
+  if (lane == 63) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wtot[wv][i] = inc[i];
+  }
+  __syncthreads();
+  if (t < (kRegionWaves + 1) * 8) {
+    const uint32_t q = t >> 3, i = t & 7u;
+    uint32_t before = 0;
+    for (uint32_t r = 0; r < q; ++r) before += wtot[r][i];
+    wpre[q][i] = before;  // row kRegionWaves: the block totals
+  }
+  __syncthreads();
+  // Start position of each class in this thread: class base (exclusive scan of the
+  // totals over classes) + waves before + lanes before.
+  uint32_t start[8], base = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t tot = wpre[kRegionWaves][i];
+    const uint32_t lo16 = tot & 0xFFFFu, hi16 = tot >> 16;
+    start[i] = wpre[wv][i] + inc[i] - cnt[i] + (base | ((base + lo16) << 16));
+    base += lo16 + hi16;
+  }
+  // The last round of a ragged region keeps zeros in its unused groups.
+  if ((n & 7u) != 0 && t < kRecordBytes / 4)
+    reinterpret_cast<uint32_t*>(stage)[(n / kPacketsPerWave) * (kRecordBytes / 4) + t] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRegionPer; ++k) {
+    if (first + k >= n) continue;
+    const uint32_t c = cls[k];
+    uint32_t sw = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) sw = (c >> 1) == i ? start[i] : sw;
+    const uint32_t q = ((sw >> (16u * (c & 1u))) & 0xFFFFu) + rank[k];
+    uint8_t* r = stage + (q / kPacketsPerWave) * kRecordBytes;
+    const uint32_t g = q % kPacketsPerWave;
+    reinterpret_cast<uint64_t*>(r)[g] = sa[k];
+    reinterpret_cast<uint32_t*>(r + kRecLenOff)[g] = len[k];
+    reinterpret_cast<uint32_t*>(r + kRecIdOff)[g] = (uint32_t)(lo + first + k);
+  }
+  __syncthreads();
+  const uint32_t words = (n + kPacketsPerWave - 1) / kPacketsPerWave * (kRecordBytes / 16);
+  u32x4* dst = reinterpret_cast<u32x4*>(recs + lo / kPacketsPerWave * kRecordBytes);
+  const u32x4* src = reinterpret_cast<const u32x4*>(stage);
+  for (uint32_t i = t; i < words; i += kRegionBlock) dst[i] = src[i];
+}
+
 // Uniform batches: base and stride multiples of 4, so every packet has the same
 // geometry relative to its own start.
 struct UniformBatch {
@@ -1056,7 +1172,8 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 
 // ---------------------------------------------------------------------------------
 // Ragged kernel, LDS-DMA form.  Packets come sorted by step class (round records from
-// crc32_class_records_kernel), so the 8 packets of a round need (nearly) the same
+// crc32_region_records_kernel, or crc32_class_records_kernel for ENET_CRC_RAGGED=global),
+// so the 8 packets of a round need (nearly) the same
 // number of slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the
 // packets with fewer steps read the zero chunk in their leading slots.  Same ring,
 // dispatch and waits as crc32_uniform_dma_kernel, with per-round, per-lane geometry
@@ -1071,6 +1188,7 @@ struct RaggedDmaBatch {
   uint64_t base;        // caller's buffer (fallback bound)
   const uint8_t* recs;  // round records
   uint64_t count;
+  uint32_t xcd_rounds;  // grid multiple of 8: sweep s of XCD x = one contiguous record range
 };
 
 struct RaggedRound {
@@ -1201,8 +1319,19 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
 
   const uint64_t total_rounds = (b.count + kPacketsPerWave - 1) / kPacketsPerWave;
   const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  // Round of this workgroup's d-th dispatch; increasing in d, a bijection over the grid.
+  // xcd_rounds: workgroup 8 j + x (dispatched to XCD x) takes, in sweep s, the W rounds at
+  // position (j + s) mod J (J = grid / 8) of the range [s sweep + x sweep/8, + sweep/8),
+  // i.e. of the region of crc32_region_records_kernel for XCD x and sweep s.  A region is
+  // sorted by step count, so a fixed position would give workgroup 0 the shortest packets
+  // of every region; the rotation gives every workgroup every position in turn.
+  const uint32_t xcd_j = blockIdx.x >> 3, xcd_nj = gridDim.x >> 3;
+  const uint64_t xcd_base = (uint64_t)(blockIdx.x & 7u) * (sweep / 8);
   auto round_of = [&](uint32_t d) -> uint64_t {
-    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+    const uint32_t s = d / kWavesPerBlock;
+    if (b.xcd_rounds)
+      return (uint64_t)s * sweep + xcd_base + (uint64_t)((xcd_j + s) % xcd_nj) * kWavesPerBlock + d % kWavesPerBlock;
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)s * sweep;
   };
   auto dma_record = [&](uint64_t rnd, uint32_t buf) {
     const uint64_t r = rnd < total_rounds ? rnd : total_rounds - 1;
@@ -2180,8 +2309,8 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
   Batch<true> b{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count};
-  // Default: the whole batch sorted by step class (histogram + records kernels), then
-  // the round DMA kernel.  ENET_CRC_RAGGED=flat: the flat-stream kernels (prep, main,
+  // Default: regions of the batch sorted by step class (region records kernel), then
+  // the round DMA kernel; =global: the whole batch sorted (histogram + records kernels).  ENET_CRC_RAGGED=flat: the flat-stream kernels (prep, main,
   // finish; the finish launch runs the streaming kernel's rounds for a batch the prep
   // kernel refused); =flatonly the same WITHOUT the fallback rounds (tests and A/B runs
   // on batches known to be in address order; any other batch leaves `out` undefined);
@@ -2194,6 +2323,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     if (v && strcmp(v, "groups") == 0) return 0;
     if (v && strcmp(v, "flat") == 0) return 3;
     if (v && strcmp(v, "flatonly") == 0) return 4;
+    if (v && strcmp(v, "global") == 0) return 5;
     return 1;
   }();
   if (count > 0xFFFFFFFFull || (ragged_mode != 0 && count < kSortMinPackets)) {
@@ -2209,7 +2339,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     return hipGetLastError();
   }
   const bool stream_kernel = ragged_mode == 2;
-  if (ragged_mode >= 3) {
+  if (ragged_mode == 3 || ragged_mode == 4) {
     // Flat path: prep, main, finish (whose blocks run the streaming kernel's rounds
     // instead when the prep kernel refused the batch).  Regions = groups of the main
     // kernel's grid (128 per workgroup, at most one workgroup per CU, about two packets
@@ -2244,6 +2374,28 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     const hipError_t ferr = hipFreeAsync(scratch, stream);
     return err != hipSuccess ? err : ferr;
   }
+  if (ragged_mode == 1) {
+    // Region records + the round DMA kernel with XCD-aligned rounds (grid multiple of 8).
+    const bool xcd = blocks % 8 == 0 && (uint64_t)blocks * kWavesPerBlock <= kRegionMax;
+    const uint32_t region = xcd ? blocks * kWavesPerBlock : kRegionMax;
+    const uint64_t nregions = (count + region - 1) / region;
+    const uint64_t rounds = (count + kPacketsPerWave - 1) / kPacketsPerWave;
+    void* scratch = nullptr;
+    hipMemPool_t pool = nullptr;
+    err = scratch_pool(&pool);
+    if (err != hipSuccess) return err;
+    err = hipMallocFromPoolAsync(&scratch, (size_t)rounds * kRecordBytes, pool, stream);
+    if (err != hipSuccess) return err;
+    uint8_t* recs = static_cast<uint8_t*>(scratch);
+    hipLaunchKernelGGL(crc32_region_records_kernel, dim3((unsigned)nregions), dim3(kRegionBlock), 0, stream, b,
+                       region, recs);
+    const RaggedDmaBatch rb{b.base, recs, count, xcd ? 1u : 0u};
+    hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
+    err = hipGetLastError();
+    const hipError_t ferr = hipFreeAsync(scratch, stream);
+    return err != hipSuccess ? err : ferr;
+  }
+  // ENET_CRC_RAGGED=global or =stream: the whole batch sorted by class.
   // >= 4096 packets per sort block: every records/scatter block reads the whole
   // histogram (16 x sort_blocks entries) to find its output positions.
   uint64_t sort_blocks = (count + 16 * kSortBlock - 1) / (16 * kSortBlock);
@@ -2270,7 +2422,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   } else {
     hipLaunchKernelGGL(crc32_class_records_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
                        (const uint32_t*)hist, second);
-    const RaggedDmaBatch rb{b.base, second, count};
+    const RaggedDmaBatch rb{b.base, second, count, 0u};
     hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
     err = hipGetLastError();
   }

@@ -234,7 +234,7 @@ def test_per_call_65_slices(dev):
 
 # --- the alternative ragged kernels (ENET_CRC_RAGGED), same oracle --------------------------
 
-@pytest.mark.parametrize("mode", ["groups", "stream"])
+@pytest.mark.parametrize("mode", ["groups", "stream", "global"])
 def test_alternative_ragged_kernels(dev, mode, monkeypatch):
     monkeypatch.setenv("ENET_CRC_RAGGED", mode)
     lens, offs, pos = [], [], 0
@@ -250,4 +250,21 @@ def test_alternative_ragged_kernels(dev, mode, monkeypatch):
     lengths = ragged_lengths(ENET_SEED + 5, 200_000, lo=0, hi=4096)
     offsets = packed_offsets(lengths) + np.uint64(1)
     data = splitmix64_bytes(13, int(lengths.sum()) + 8)
+    assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
+
+
+# --- region sort (default ragged pre-pass): region sizes and grids around its edges ----------
+
+@pytest.mark.parametrize("count", [4096, 4100, 5000, 8 * 4096 + 3, 70_001])
+def test_ragged_region_sort_edges(dev, count):
+    # 4096: the smallest sorted batch; 4100: a grid of 33 workgroups (not a multiple of 8,
+    # so 4096-packet regions and the plain round order); 5000: 40 workgroups (XCD-aligned
+    # regions of 640); the others end in a partial region and a partial round.  Lengths
+    # 0..3000 so every region mixes step classes (empty packets included), unaligned starts.
+    rng = np.random.default_rng(count)
+    lengths = rng.integers(0, 3001, size=count).astype(np.uint32)
+    lengths[rng.integers(0, count, size=count // 50)] = 0
+    gaps = rng.integers(0, 4, size=count).astype(np.uint64)
+    offsets = (packed_offsets(lengths) + np.cumsum(gaps)).astype(np.uint64) + np.uint64(3)
+    data = splitmix64_bytes(count + 1, int(offsets[-1] + lengths[-1]) + 8)
     assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
