@@ -253,10 +253,10 @@ __device__ __forceinline__ void load_top_words(uint64_t chunk_addr, uint32_t met
       : "memory");
 }
 
-// Combine the 4 word streams of each of the group's 8 lanes into the packet's
-// register (before trailing bytes).  Valid on lane k == 0 of the group.
-__device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
-                                                   uint32_t h3, const Lookup& lk) {
+// Combine the 4 word streams of each of the group's 8 lanes into y, the packet's
+// register before the shift of its last word (register = M32 y).  Valid on lane k == 0.
+__device__ __forceinline__ uint32_t combine_tree(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
+                                                uint32_t h3, const Lookup& lk) {
   // In-lane Horner over the 4 word slots with M32^1 (replicated: conflict-free).
   uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
   y = apply_rep(lds, y, h2, lk.lp1, lk);
@@ -271,7 +271,33 @@ __device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_
   y ^= from_lane_plus<2>(t);
   if (k == 4u) t = apply_small(lds + kTreeDword + 2048, y);
   y ^= from_lane_plus<4>(t);
+  return y;
+}
+
+// The packet's register (before trailing bytes), valid on lane k == 0 of the group.
+__device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
+                                                   uint32_t h3, const Lookup& lk) {
+  const uint32_t y = combine_tree(lds, h0, h1, h2, h3, lk);
   return apply_rep(lds, y, 0u, lk.lp1, lk);  // every lane (conflict-free); lane k == 0 holds the register
+}
+
+// The register of a packet the DMA kernels ran z = 0..3 zero bytes past its end (to the
+// next 4-byte boundary), from the tree value y: M8^-z M32 y = M8^m y with m = 4 - z, so
+// the last word's shift simply stops z bytes short.  With table t of the M32^1 set being
+// M8^(4-t) of one byte:  M8^m(y) = (y >> 8m) ^ sum_{j<m} table(4-m+j)[byte j of y].
+// One round of <= 4 independent lookups instead of M32 plus 2z dependent ones (the
+// inverse zero-byte steps through inv_top used before).  Call on lanes k == 0 only: copy = group, so the
+// 8 lanes of a wave never share a bank.
+__device__ __forceinline__ uint32_t finish_word(const uint32_t* lds, uint32_t y, uint32_t z) {
+  const uint32_t m = 4u - z, copy = (threadIdx.x >> 3) & 7u;
+  uint32_t r = m < 4u ? y >> (8u * m) : 0u;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t t = 4u - m + j;  // >= 4: byte j is shifted out entirely
+    const uint32_t v = lds[((y >> (8u * j)) & 0xFFu) * kRowDwords + kSetM1Bytes / 4 + (t & 3u) * kRepCopies + copy];
+    r ^= t < 4u ? v : 0u;
+  }
+  return r;
 }
 
 // Sarwate byte steps (src/crc32.rs:43) over `ntail` bytes of `word` from byte `tsh`.
@@ -280,21 +306,6 @@ __device__ __forceinline__ uint32_t tail_steps(const uint32_t* lds, uint32_t reg
 #pragma unroll
   for (uint32_t t = 0; t < 3; ++t) {
     if (t < ntail) reg = (reg >> 8) ^ sarwate_at(lds, (reg ^ (word >> (8u * (tsh + t)))) & 0xffu);
-  }
-  return reg;
-}
-
-// Undo z zero-byte steps (z <= 3): the DMA kernels run every packet to the next
-// 4-byte boundary, with the z bytes past its end masked to zero, which leaves
-// M8^z(reg) in the register; M8^-1 recovers the table index from the top byte.
-__device__ __forceinline__ uint32_t unshift_zero_bytes(const uint32_t* lds, uint32_t reg, uint32_t z) {
-  const uint8_t* inv_top = reinterpret_cast<const uint8_t*>(lds + kInvTopDword);
-#pragma unroll
-  for (uint32_t t = 0; t < 3; ++t) {
-    if (t < z) {
-      const uint32_t idx = inv_top[reg >> 24];
-      reg = ((reg ^ sarwate_at(lds, idx)) << 8) | idx;
-    }
   }
   return reg;
 }
@@ -914,8 +925,8 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 //
 // Trailing bytes: every packet is run to the next 4-byte boundary (Lx = length
 // rounded up), the z = Lx - length bytes past its end are masked to zero in the last
-// word (lane 0's last slot), and z inverse zero-byte steps after the combine undo
-// them (unshift_zero_bytes).  No separate tail-word load.
+// word (lane 0's last slot), and the combine's last-word shift stops z bytes short
+// (finish_word).  No separate tail-word load.
 template <int NS>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   constexpr int kDmaRing = kUniformRing;
@@ -1033,8 +1044,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
       for (int32_t s = 1; s < ns - 1; ++s) slot(s, false, false);
       slot(ns - 1, false, true);
     }
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
-    if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);
+    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+    uint32_t reg = 0;
+    if (c.k == 0) reg = finish_word(lds, y, z);
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     // Lane 8g+j keeps the checksum of group g in this wave's j-th round of 8; one store per 8.
     if (c.k == j) {
@@ -1151,8 +1163,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
       q[s] = load_chunk(slot_src(pbn, s));  // the next round's slot s
       issue_order_fence();
     }
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
-    if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);
+    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+    uint32_t reg = 0;
+    if (c.k == 0) reg = finish_word(lds, y, z);
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
       res = crc;
@@ -1182,13 +1195,14 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 // lanes 32-63 duplicate it), issued two rounds ahead and read with ds_read at the
 // previous round's end, at least kDmaRing-1 DMAs later.  Trailing bytes as in the
 // uniform DMA kernel: each packet runs to the next 4-byte boundary with the bytes
-// past its end masked, then unshift_zero_bytes.
+// past its end masked, then finish_word.
 // ---------------------------------------------------------------------------------
 struct RaggedDmaBatch {
   uint64_t base;        // caller's buffer (fallback bound)
   const uint8_t* recs;  // round records
   uint64_t count;
   uint32_t xcd_rounds;  // grid multiple of 8: sweep s of XCD x = one contiguous record range
+  uint32_t top0_only;   // ENET_CRC_FASTTOP=0: short-packet rounds take the generic path (A/B)
 };
 
 struct RaggedRound {
@@ -1199,7 +1213,8 @@ struct RaggedRound {
   uint32_t id;          // packet id (output index)
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
   bool direct;          // top chunk read directly (not fallback / not before the packet)
-  bool fast;            // wave-uniform: every lane's top is slot 0, no fallback, ns <= kRaggedFastMax
+  bool fast;            // wave-uniform: every lane's top is the same slot, no fallback, ns <= kRaggedFastMax
+  int32_t top_uniform;  // that slot (0 unless ns == kRaggedRing and the packets are shorter)
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
@@ -1237,21 +1252,29 @@ struct RaggedRing {
   __device__ __forceinline__ uint32_t next_addr() const { return ring0 + q * kRingStride + lane16; }
 };
 
-// A round in which every packet has exactly NS steps and needs no fallback: the slot
-// loop of crc32_uniform_dma_kernel (unrolled, lookups fused with the next ring read);
-// slot 0 masks the top words, the last slot the bytes past each packet's end.
-template <int NS>
+// A round in which every packet has the same step count and needs no fallback: the
+// slot loop of crc32_uniform_dma_kernel (unrolled, lookups fused with the next ring
+// read); slot T (the packets' top slot) masks the top words, the last slot the bytes
+// past each packet's end.  T > 0 only for rounds of packets shorter than the ring
+// (NS = kRaggedRing): their first T slots hold zero chunks and are only consumed.
+template <int NS, int T = 0>
 __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
                                                   const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
                                                   uint32_t& h3) {
+  static_assert(T == 0 || NS == kRaggedRing, "leading zero slots only in ring-length rounds");
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const u32x4 v = R.nextv;
     const int32_t f = s + kRaggedRing;  // refill this slot's LDS slot kRaggedRing slots ahead
     R.dma(f < NS ? cur.cb + (uint64_t)kBytesPerStep * (uint64_t)f : ragged_src(nxt, f - NS, c.dummy));
+    if (s < T) {
+      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
+      issue_order_fence();
+      continue;
+    }
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     if (s == NS - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
-    if (s == 0) {
+    if (s == T) {
       if (__builtin_amdgcn_ballot_w64(cur.meta & kMetaHeadMask)) {
         if (cur.meta & kMetaHeadMask) mask_top(cur.meta, w0, w1, w2, w3);
       }
@@ -1271,8 +1294,17 @@ template <int... I>
 __device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRound& cur, const RaggedRound& nxt,
                                                       RaggedRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                       uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
-  return ((ns == I + kRaggedRing ? (ragged_round_fast<I + kRaggedRing>(cur, nxt, R, c, h0, h1, h2, h3), true)
-                                 : false) || ...);
+  if (ns == kRaggedRing) {
+    switch (cur.top_uniform) {
+      case 0: ragged_round_fast<kRaggedRing, 0>(cur, nxt, R, c, h0, h1, h2, h3); return true;
+      case 1: ragged_round_fast<kRaggedRing, 1>(cur, nxt, R, c, h0, h1, h2, h3); return true;
+      case 2: ragged_round_fast<kRaggedRing, 2>(cur, nxt, R, c, h0, h1, h2, h3); return true;
+      case 3: ragged_round_fast<kRaggedRing, 3>(cur, nxt, R, c, h0, h1, h2, h3); return true;
+      default: return false;
+    }
+  }
+  return ((ns == I + kRaggedRing + 1 ? (ragged_round_fast<I + kRaggedRing + 1>(cur, nxt, R, c, h0, h1, h2, h3), true)
+                                     : false) || ...);
 }
 
 // Any round (mixed step counts, fallback chunks, long packets): per-lane top slot.
@@ -1358,11 +1390,12 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
     rr.meta = round_meta(g, c.k, c.base4, valid, unused_tail, c.dummy) | (z << kMetaNTailShift);
     rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
     rr.id = id;
-    // Fast: every packet starts at slot 0 (same step count), no fallback chunk, and the
-    // lanes whose top chunk lies before their packet are exactly the ones the round
-    // reads as zeros (ragged_src with top_slot 0 and !direct).
-    rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != 0 || (rr.meta & kMetaFallback)) &&
-              rr.ns <= kRaggedFastMax;
+    // Fast: every packet starts at the same slot (same step count), no fallback chunk,
+    // and the lanes whose top chunk lies before their packet are exactly the ones the
+    // round reads as zeros (ragged_src with !direct).
+    rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
+    rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform || (rr.meta & kMetaFallback)) &&
+              rr.ns <= kRaggedFastMax && !(b.top0_only && rr.top_uniform != 0);
     return rr;
   };
 
@@ -1393,13 +1426,13 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     if (!cur.fast ||
         !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
-                               std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing + 1>{}))
+                               std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
       ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
     // Round end (record rnd[2] has landed: >= kDmaRing-1 DMAs since it was issued).
-    uint32_t reg = combine_streams(lds, h0, h1, h2, h3, c.lk);
+    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+    uint32_t reg = 0;
+    if (c.k == 0) reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u);
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
-    const uint32_t z = (cur.meta >> kMetaNTailShift) & 3u;
-    if (z != 0 && c.k == 0) reg = unshift_zero_bytes(lds, reg, z);
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
       res = crc;
@@ -1648,8 +1681,9 @@ __global__ __launch_bounds__(kBlock) void crc32_group_stream_kernel(GsBatch batc
     const u32x4 hv = S.park[wv][row][lane];
     const uint32_t col = lane >> 3;
     const uint32_t id = S.pmeta[wv][row][col][0], z = S.pmeta[wv][row][col][1];
-    uint32_t reg = combine_streams(lds, hv.x, hv.y, hv.z, hv.w, c.lk);
-    if (z != 0 && k == 0) reg = unshift_zero_bytes(lds, reg, z);
+    const uint32_t y = combine_tree(lds, hv.x, hv.y, hv.z, hv.w, c.lk);
+    uint32_t reg = 0;
+    if (k == 0) reg = finish_word(lds, y, z);
     if (k == 0 && col < ncols) out[id] = __builtin_bswap32(~reg);
   };
 
@@ -2389,7 +2423,8 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     uint8_t* recs = static_cast<uint8_t*>(scratch);
     hipLaunchKernelGGL(crc32_region_records_kernel, dim3((unsigned)nregions), dim3(kRegionBlock), 0, stream, b,
                        region, recs);
-    const RaggedDmaBatch rb{b.base, recs, count, xcd ? 1u : 0u};
+    const char* ft = getenv("ENET_CRC_FASTTOP");
+    const RaggedDmaBatch rb{b.base, recs, count, xcd ? 1u : 0u, (ft && strcmp(ft, "0") == 0) ? 1u : 0u};
     hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
     err = hipGetLastError();
     const hipError_t ferr = hipFreeAsync(scratch, stream);
@@ -2422,7 +2457,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   } else {
     hipLaunchKernelGGL(crc32_class_records_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
                        (const uint32_t*)hist, second);
-    const RaggedDmaBatch rb{b.base, second, count, 0u};
+    const RaggedDmaBatch rb{b.base, second, count, 0u, 0u};
     hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
     err = hipGetLastError();
   }

@@ -5,7 +5,8 @@
 // head masking / init injection and the fixed-shift combine tree for every lane
 // count the kernel template allows, without a GPU.  kExt models the LDS-DMA kernels'
 // trailing-byte handling: the packet runs to the next 4-byte boundary with the bytes
-// past its end masked to zero, then z inverse zero-byte steps (via inv_top).
+// past its end masked to zero, and the last word's shift stops z bytes short
+// (finish_word: M8^(4-z) y from the M32^1 tables, instead of M32 y).
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -69,14 +70,16 @@ static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
       for (int k = 0; k < G; ++k) t[k] = op(l + 1, y[k]);
       for (int k = 0; k + d < G; ++k) y[k] ^= t[k + d];
     }
-    reg = op(0, y[0]);
-  }
-  if constexpr (kExt) {
-    for (uint64_t t = 0; t < z; ++t) {  // M8^-1: the table index from the top byte
-      const uint32_t idx = T.inv_top[reg >> 24];
-      reg = ((reg ^ T.sarwate[idx]) << 8) | idx;
+    if (kExt) {
+      // finish_word: M8^m(y) = (y >> 8m) ^ sum_{j<m} op[0][4-m+j][byte j of y], m = 4 - z.
+      const uint32_t m = 4 - (uint32_t)z;
+      reg = m < 4 ? y[0] >> (8 * m) : 0u;
+      for (uint32_t j = 0; j < m; ++j) reg ^= T.op[0][4 - m + j][(y[0] >> (8 * j)) & 0xffu];
+    } else {
+      reg = op(0, y[0]);
     }
-  } else {
+  }
+  if constexpr (!kExt) {
     for (uint64_t b = (a1 > sa ? a1 : sa); b < ea; ++b) reg = (reg >> 8) ^ T.sarwate[(reg ^ buf[b]) & 0xffu];
   }
   return __builtin_bswap32(~reg);
