@@ -64,8 +64,9 @@ typedef struct enet_crc_ctx enet_crc_ctx;
 /* Per-call modes of enet_crc32_iov (enet_crc_ctx_set_percall_mode). */
 #define ENET_CRC_PERCALL_COPY 0     /* pinned staging -> H2D copy -> kernel -> D2H copy */
 #define ENET_CRC_PERCALL_ZEROCOPY 1 /* kernel reads mapped pinned memory, writes the result to it */
-/* (default) A server wave stays resident on lane 0's device and polls a mailbox in
- * pinned host memory: no kernel launch per call.  It exits 20 ms after the last call
+/* (default) A server wave stays resident on lane 0's device and polls a request mailbox
+ * (device memory the host writes through the PCIe BAR on large-BAR devices, else pinned
+ * host memory; answers in pinned host memory): no kernel launch per call.  It exits 20 ms after the last call
  * (the next call relaunches it) and holds one CU while it runs; the context's batch
  * entry points stop it first.  Datagrams above 4096 B take the zero-copy path. */
 #define ENET_CRC_PERCALL_PERSISTENT 2

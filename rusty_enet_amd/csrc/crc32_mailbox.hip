@@ -10,9 +10,10 @@
 // register of the window; the host adds M8^len(0xFFFFFFFF) and finishes bswap32(~reg)
 // (src/crc32.rs:39-47).
 //
-// Every access to the mailbox is a vector load or store with system scope (sc0 sc1) in
+// Every access to the mailboxes is a vector load or store with system scope (sc0 sc1) in
 // inline asm, so nothing is cached between polls and each store has reached host memory
-// before the next one is issued (s_waitcnt vmcnt(0)).
+// before the next one is issued (s_waitcnt vmcnt(0)).  Requests are read from `req`,
+// answers written to `resp` (crc32_mailbox.hpp).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -78,24 +79,33 @@ __device__ __forceinline__ uint32_t apply4(const uint32_t* t, uint32_t x) {
 
 constexpr int kMbLevels = 6;  // 64 chunks
 
-__global__ __launch_bounds__(64) void crc32_mailbox_kernel(Mailbox* mb, const uint32_t* __restrict__ ladder) {
+// Value of lane + d (d = 1, 2, 4, 8) inside a 16-lane row, through DPP: no LDS round trip.
+template <int D>
+__device__ __forceinline__ uint32_t from_lane_down(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + D, 0xf, 0xf, true);  // row_shl:D
+}
+
+__global__ __launch_bounds__(64) void crc32_mailbox_kernel(const Mailbox* req, Mailbox* resp,
+                                                           const uint32_t* __restrict__ ladder) {
   __shared__ uint32_t m32[kSlotLevelDwords];               // ladder level 0: M32
+  __shared__ uint32_t m32x2[kSlotLevelDwords];             // ladder level 1: M32^2
   __shared__ uint32_t m32x4[kSlotLevelDwords];             // ladder level 2: M32^4
   __shared__ uint32_t lv[kMbLevels][kSlotLevelDwords];     // ladder levels 4 .. 9
   const uint32_t lane = threadIdx.x;
   for (uint32_t x = lane; x < kSlotLevelDwords; x += 64) {
     m32[x] = ladder[x];
+    m32x2[x] = ladder[kSlotLevelDwords + x];
     m32x4[x] = ladder[2 * kSlotLevelDwords + x];
 #pragma unroll
     for (int k = 0; k < kMbLevels; ++k) lv[k][x] = ladder[(4 + k) * kSlotLevelDwords + x];
   }
   __syncthreads();
-  uint32_t last = __builtin_amdgcn_readfirstlane(sys_load(&mb->done));
+  uint32_t last = __builtin_amdgcn_readfirstlane(sys_load(&resp->done));
   const uint64_t t0 = wall_clock64();
   uint64_t t_last = t0;
   for (;;) {
     uint32_t seq, len;
-    sys_load2(&mb->seq, seq, len);  // one 64-bit word: the host posts both with one store
+    sys_load2(&req->seq, seq, len);  // one 64-bit word: the host posts both with one store
     seq = __builtin_amdgcn_readfirstlane(seq);
     len = __builtin_amdgcn_readfirstlane(len);
     if (seq == kMailboxStop) break;
@@ -108,30 +118,41 @@ __global__ __launch_bounds__(64) void crc32_mailbox_kernel(Mailbox* mb, const ui
     const uint32_t first_chunk = (kMailboxBytes - (len < kMailboxBytes ? len : kMailboxBytes)) / 64u;
     uint32_t r = 0;
     if (lane >= first_chunk) {
-      const uint8_t* src = mb->data + 64u * lane;
+      const uint8_t* src = req->data + 64u * lane;
       u32x4m v[4];
       sys_load64(src, v[0], v[1], v[2], v[3]);
-      // Four interleaved word streams (word 4i + j in stream j, steps of M32^4), then
-      // one M32 Horner over the four: 4 + 3 dependent lookup rounds instead of 16.
-      uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+      // Four interleaved word streams (word 4i + j in stream j, steps of M32^4; the first
+      // step from a zero register is free), then the chunk register including the last
+      // word's own step, r = M^4 a0 ^ M^3 a1 ^ M^2 a2 ^ M a3 = M^4 a0 ^ M a3 ^ M^2 (M a1 ^ a2)
+      // (M = M32): 3 + 2 dependent lookup rounds instead of 16.
+      uint32_t a0 = v[0].x, a1 = v[0].y, a2 = v[0].z, a3 = v[0].w;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 1; i < 4; ++i) {
         a0 = apply4(m32x4, a0) ^ v[i].x;
         a1 = apply4(m32x4, a1) ^ v[i].y;
         a2 = apply4(m32x4, a2) ^ v[i].z;
         a3 = apply4(m32x4, a3) ^ v[i].w;
       }
-      r = apply4(m32, a0) ^ a1;
-      r = apply4(m32, r) ^ a2;
-      r = apply4(m32, r) ^ a3;
-      r = apply4(m32, r);  // the last word's own step: reg = M32(reg ^ w)
+      const uint32_t t = apply4(m32, a1) ^ a2;
+      r = apply4(m32x4, a0) ^ apply4(m32, a3) ^ apply4(m32x2, t);
     }
-#pragma unroll
-    for (int k = 0; k < kMbLevels; ++k) {
-      const uint32_t right = (uint32_t)__shfl_down((int)r, 1 << k, 64);
-      if ((lane & ((2u << k) - 1u)) == 0) r = apply4(lv[k], r) ^ right;
+    // Tree over the 64 chunk registers; level k moves lane + 2^k's value (DPP inside a
+    // 16-lane row for k < 4, a shuffle across rows for the last two levels).
+    {
+      uint32_t right = from_lane_down<1>(r);
+      if ((lane & 1u) == 0) r = apply4(lv[0], r) ^ right;
+      right = from_lane_down<2>(r);
+      if ((lane & 3u) == 0) r = apply4(lv[1], r) ^ right;
+      right = from_lane_down<4>(r);
+      if ((lane & 7u) == 0) r = apply4(lv[2], r) ^ right;
+      right = from_lane_down<8>(r);
+      if ((lane & 15u) == 0) r = apply4(lv[3], r) ^ right;
+      right = (uint32_t)__shfl_down((int)r, 16, 64);
+      if ((lane & 31u) == 0) r = apply4(lv[4], r) ^ right;
+      right = (uint32_t)__shfl_down((int)r, 32, 64);
+      if (lane == 0) r = apply4(lv[5], r) ^ right;
     }
-    if (lane == 0) sys_store2(&mb->done, seq, r);  // done and result in one 64-bit store
+    if (lane == 0) sys_store2(&resp->done, seq, r);  // done and result in one 64-bit store
     last = seq;
     t_last = now;
   }
@@ -139,8 +160,8 @@ __global__ __launch_bounds__(64) void crc32_mailbox_kernel(Mailbox* mb, const ui
 
 }  // namespace
 
-hipError_t launch_mailbox(Mailbox* mb, const uint32_t* ladder, hipStream_t stream) {
-  hipLaunchKernelGGL(crc32_mailbox_kernel, dim3(1), dim3(64), 0, stream, mb, ladder);
+hipError_t launch_mailbox(const Mailbox* req, Mailbox* resp, const uint32_t* ladder, hipStream_t stream) {
+  hipLaunchKernelGGL(crc32_mailbox_kernel, dim3(1), dim3(64), 0, stream, req, resp, ladder);
   return hipGetLastError();
 }
 

@@ -1,7 +1,8 @@
 // Persistent per-call checksum server (ENET_CRC_PERCALL_PERSISTENT, enet_crc32_iov):
-// one wave polls a mailbox in pinned, coherent host memory, checksums each datagram
-// the host posts there and writes the register back, so a call costs PCIe round trips
-// instead of a kernel launch plus a stream synchronisation.  Shared by
+// one wave polls a request mailbox (in device memory the host writes through the BAR, or
+// in pinned host memory), checksums each datagram the host posts there and writes the
+// register back into pinned host memory, so a call costs PCIe transfers instead of a
+// kernel launch plus a stream synchronisation.  Shared by
 // crc32_mailbox.hip (the kernel) and enet_crc_abi.hip (the host side).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -28,9 +29,12 @@ struct alignas(128) Mailbox {
                                 // holding the first byte is zero below it
 };
 
-// Starts the server wave on `stream` (`mb` is the device address of the mailbox,
-// `ladder` the device ladder of crc32_slot.hpp).  The kernel returns on kMailboxStop,
-// after kMailboxIdleTicks without a request, or after kMailboxMaxTicks.
-hipError_t launch_mailbox(Mailbox* mb, const uint32_t* ladder, hipStream_t stream);
+// Starts the server wave on `stream`.  `req` is the device address of the mailbox the
+// requests are read from (seq, len, data: fine-grained device memory the host writes
+// through the PCIe BAR when the device has a large BAR, else pinned host memory), `resp`
+// that of the one the answers go to (done, result: always pinned host memory, where the
+// host polls); `ladder` is the device ladder of crc32_slot.hpp.  The kernel returns on
+// kMailboxStop, after kMailboxIdleTicks without a request, or after kMailboxMaxTicks.
+hipError_t launch_mailbox(const Mailbox* req, Mailbox* resp, const uint32_t* ladder, hipStream_t stream);
 
 }  // namespace enet_crc

@@ -238,8 +238,11 @@ struct PerCall {
   uint8_t* h_in = nullptr;
   size_t cap = 0;
   uint32_t* h_res = nullptr;  // [0] = checksum (mapped: written by the kernel)
-  Mailbox* mb = nullptr;      // host address of the mailbox
+  Mailbox* mb = nullptr;      // host address of the answer mailbox (pinned host memory)
   Mailbox* d_mb = nullptr;    // its device address
+  Mailbox* req = nullptr;     // host address of the request mailbox
+  Mailbox* d_req = nullptr;   // its device address
+  bool req_vram = false;      // request mailbox in device memory written through the BAR
   hipStream_t mb_stream = nullptr;
   bool mb_launched = false;   // a server was launched and may still run
   uint32_t mb_seq = 0;        // last request number posted
@@ -534,7 +537,8 @@ namespace {
 // Ask a running server to exit and wait until it has (its stream drains).
 void stop_mailbox(PerCall& c) {
   if (!c.mb_launched) return;
-  __atomic_store_n(&c.mb->seq, kMailboxStop, __ATOMIC_RELEASE);
+  __atomic_store_n(&c.req->seq, kMailboxStop, __ATOMIC_RELEASE);
+  __builtin_ia32_sfence();
   (void)hipStreamSynchronize(c.mb_stream);
   c.mb_launched = false;
 }
@@ -573,6 +577,7 @@ void enet_crc_ctx_destroy(enet_crc_ctx* ctx) {
     DeviceGuard g(ctx->lanes[0].device);
     if (ctx->call.h_in) (void)hipHostFree(ctx->call.h_in);
     if (ctx->call.h_res) (void)hipHostFree(ctx->call.h_res);
+    if (ctx->call.req && ctx->call.req_vram) (void)hipFree(ctx->call.d_req);
     if (ctx->call.mb) (void)hipHostFree(ctx->call.mb);
     if (ctx->call.mb_stream) (void)hipStreamDestroy(ctx->call.mb_stream);
   }
@@ -679,11 +684,29 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
       memset(c.mb, 0, sizeof(Mailbox));
       ENET_HIP_TRY(hipHostGetDevicePointer((void**)&c.d_mb, c.mb, 0));
       ENET_HIP_TRY(hipStreamCreateWithFlags(&c.mb_stream, hipStreamNonBlocking));
+      // Requests: in fine-grained device memory that the host writes through the PCIe BAR
+      // when the whole VRAM is host-visible (large BAR), so the server reads each
+      // datagram locally instead of across PCIe; otherwise the answer
+      // mailbox doubles as the request mailbox.  ENET_CRC_MAILBOX=host forces the latter.
+      int large_bar = 0;
+      const char* mv = getenv("ENET_CRC_MAILBOX");
+      if (!(mv && strcmp(mv, "host") == 0) &&
+          hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, L.device) == hipSuccess && large_bar &&
+          hipExtMallocWithFlags((void**)&c.d_req, sizeof(Mailbox), hipDeviceMallocFinegrained) == hipSuccess) {
+        c.req = c.d_req;  // one address for host and device
+        c.req_vram = true;
+        memset(c.req, 0, sizeof(Mailbox));
+        __builtin_ia32_sfence();
+      } else {
+        (void)hipGetLastError();
+        c.req = c.mb;
+        c.d_req = c.d_mb;
+      }
     }
     const uint32_t* ladder = nullptr;
     ENET_HIP_TRY(device_slot_ladder(&ladder));
-    uint8_t* dst = c.mb->data + (kMailboxBytes - total);  // right-aligned; zero below it in its chunk
-    memset(c.mb->data + ((kMailboxBytes - total) & ~(size_t)63), 0, (kMailboxBytes - total) & 63);
+    uint8_t* dst = c.req->data + (kMailboxBytes - total);  // right-aligned; zero below it in its chunk
+    memset(c.req->data + ((kMailboxBytes - total) & ~(size_t)63), 0, (kMailboxBytes - total) & 63);
     size_t pos = 0;  // concatenation, src/crc32.rs:41-42
     for (size_t i = 0; i < nbufs; ++i) {
       if (bufs[i].len) memcpy(dst + pos, bufs[i].data, bufs[i].len);
@@ -691,10 +714,14 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
     }
     c.mb_seq = c.mb_seq + 1 == kMailboxStop ? 1u : c.mb_seq + 1;
     const uint32_t seq = c.mb_seq;
-    // seq and len in one 64-bit store, ordered after the bytes.
-    __atomic_store_n(reinterpret_cast<uint64_t*>(&c.mb->seq), ((uint64_t)total << 32) | seq, __ATOMIC_RELEASE);
+    // seq and len in one 64-bit store, ordered after the bytes.  Through the BAR the
+    // mapping is write-combining: sfence drains the bytes before the store and the store
+    // itself right after it (without it a store can sit in the buffer for milliseconds).
+    if (c.req_vram) __builtin_ia32_sfence();
+    __atomic_store_n(reinterpret_cast<uint64_t*>(&c.req->seq), ((uint64_t)total << 32) | seq, __ATOMIC_RELEASE);
+    if (c.req_vram) __builtin_ia32_sfence();
     auto launch = [&]() -> hipError_t {
-      const hipError_t e = launch_mailbox(c.d_mb, ladder, c.mb_stream);
+      const hipError_t e = launch_mailbox(c.d_req, c.d_mb, ladder, c.mb_stream);
       c.mb_launched = e == hipSuccess;
       return e;
     };
