@@ -625,39 +625,41 @@ __global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<t
 }
 
 // Round records for crc32_ragged_dma_kernel: sorted position q = 8 r + g goes to
-// record r, group g.  128 B per round: start addresses (u64 x 8), lengths (u32 x 8),
-// packet ids (u32 x 8).
+// record r, group g.  128 B per round, per group: the packet's geometry precomputed
+// (ragged_record) so the round kernel derives every lane's plan with 32-bit arithmetic,
+// and its id (the output index).
+//   bytes  0-63: u64 x 8  a1 | v << 48 | z << 50 | near << 52 | 1 << 53
+//                 a1 = end of the packet run to the next 4-byte boundary (z = 0..3 bytes
+//                 past the end), v = sa & 3, near = top within 16 B of the caller's base
+//                 (only then can a top chunk need the fallback), bit 53 = a packet is here
+//   bytes 64-95: u32 x 8  nsteps | (pad / 4) << 26, pad = 128 nsteps - 4 nwords
+//   bytes 96-127: u32 x 8 packet id
+// (GPU virtual addresses are below 2^48.)
 constexpr uint32_t kRecordBytes = 128;
-constexpr uint32_t kRecLenOff = 64, kRecIdOff = 96;
+constexpr uint32_t kRecInfoOff = 64, kRecIdOff = 96;
+constexpr uint64_t kRecAddrMask = (1ull << 48) - 1;
+constexpr int kRecVShift = 48, kRecZShift = 50, kRecNearBit = 52, kRecValidBit = 53;
+constexpr uint32_t kRecStepsMask = (1u << 26) - 1;
+constexpr int kRecPadShift = 26;
 
-__global__ __launch_bounds__(kSortBlock) void crc32_class_records_kernel(Batch<true> b, const uint32_t* __restrict__ hist,
-                                                                          uint8_t* __restrict__ recs) {
-  __shared__ uint32_t cur[kStepClasses];
-  block_class_bases(hist, cur);
-  uint64_t lo, hi;
-  sort_range(b.count, lo, hi);
-  for (uint64_t p0 = lo + threadIdx.x; p0 < hi; p0 += kSortBlock * kSortPer) {
-    uint64_t off[kSortPer];
-    uint32_t len[kSortPer];
-#pragma unroll
-    for (int k = 0; k < kSortPer; ++k) {
-      const uint64_t p = p0 + (uint64_t)k * kSortBlock;
-      off[k] = p < hi ? b.offsets[p] : 0;
-      len[k] = p < hi ? b.lengths[p] : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kSortPer; ++k) {
-      const uint64_t p = p0 + (uint64_t)k * kSortBlock;
-      if (p >= hi) continue;
-      const uint64_t sa = b.base + off[k];
-      const uint64_t q = atomicAdd(&cur[step_class_of(sa, len[k])], 1u);
-      uint8_t* r = recs + (q / kPacketsPerWave) * kRecordBytes;
-      const uint32_t g = (uint32_t)(q % kPacketsPerWave);
-      reinterpret_cast<uint64_t*>(r)[g] = sa;
-      reinterpret_cast<uint32_t*>(r + kRecLenOff)[g] = len[k];
-      reinterpret_cast<uint32_t*>(r + kRecIdOff)[g] = (uint32_t)p;
-    }
-  }
+struct RaggedRecord {
+  uint64_t ax;
+  uint32_t info;
+  uint32_t nsteps;
+};
+
+__device__ __forceinline__ RaggedRecord ragged_record(uint64_t sa, uint32_t len, uint64_t base4) {
+  const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
+  const PacketGeo g = make_geo(sa, (uint64_t)len + z);  // runs to the next 4-byte boundary
+  const uint32_t nwords = (uint32_t)((g.a1 - g.top) >> 2);
+  const uint32_t pad = 128u * (uint32_t)g.nsteps - 4u * nwords;  // 0..124
+  const uint64_t near = g.top - base4 < 16 ? 1ull : 0ull;
+  RaggedRecord r;
+  r.ax = g.a1 | ((sa & 3u) << kRecVShift) | ((uint64_t)z << kRecZShift) | (near << kRecNearBit) |
+         (1ull << kRecValidBit);
+  r.info = (uint32_t)g.nsteps | ((pad >> 2) << kRecPadShift);
+  r.nsteps = (uint32_t)g.nsteps;
+  return r;
 }
 
 // Region records (the default pre-pass): the batch in regions of R consecutive packets,
@@ -708,10 +710,14 @@ __global__ __launch_bounds__(kRegionBlock) void crc32_region_records_kernel(Batc
   // fields (class c: word c/2, half c%2).  Static indices only: a dynamically indexed
   // register array goes to scratch.
   uint32_t cls[kRegionPer], rank[kRegionPer], cnt[8];
+  const uint64_t base4 = b.base & ~(uint64_t)3;
+  uint32_t info[kRegionPer];
 #pragma unroll
   for (int k = 0; k < kRegionPer; ++k) {
-    sa[k] += b.base;
-    cls[k] = first + k < n ? step_class_of(sa[k], len[k]) : (uint32_t)kStepClasses;
+    const RaggedRecord rec = ragged_record(b.base + sa[k], len[k], base4);
+    sa[k] = rec.ax;
+    info[k] = rec.info;
+    cls[k] = first + k < n ? (rec.nsteps < kStepClasses - 1 ? rec.nsteps : kStepClasses - 1) : (uint32_t)kStepClasses;
     rank[k] = 0;
 #pragma unroll
     for (int j = 0; j < k; ++j) rank[k] += cls[j] == cls[k] ? 1u : 0u;
@@ -766,7 +772,7 @@ __global__ __launch_bounds__(kRegionBlock) void crc32_region_records_kernel(Batc
     uint8_t* r = stage + (q / kPacketsPerWave) * kRecordBytes;
     const uint32_t g = q % kPacketsPerWave;
     reinterpret_cast<uint64_t*>(r)[g] = sa[k];
-    reinterpret_cast<uint32_t*>(r + kRecLenOff)[g] = len[k];
+    reinterpret_cast<uint32_t*>(r + kRecInfoOff)[g] = info[k];
     reinterpret_cast<uint32_t*>(r + kRecIdOff)[g] = (uint32_t)(lo + first + k);
   }
   __syncthreads();
@@ -1185,8 +1191,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 
 // ---------------------------------------------------------------------------------
 // Ragged kernel, LDS-DMA form.  Packets come sorted by step class (round records from
-// crc32_region_records_kernel, or crc32_class_records_kernel for ENET_CRC_RAGGED=global),
-// so the 8 packets of a round need (nearly) the same
+// crc32_region_records_kernel), so the 8 packets of a round need (nearly) the same
 // number of slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the
 // packets with fewer steps read the zero chunk in their leading slots.  Same ring,
 // dispatch and waits as crc32_uniform_dma_kernel, with per-round, per-lane geometry
@@ -1219,15 +1224,15 @@ struct RaggedRound {
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
 
-__device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint64_t& addr, uint32_t& len,
+__device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint64_t& addr, uint32_t& info,
                                             uint32_t& id) {
-  const uint32_t a = rec_lds + 8u * grp, l = rec_lds + kRecLenOff + 4u * grp, i = rec_lds + kRecIdOff + 4u * grp;
+  const uint32_t a = rec_lds + 8u * grp, l = rec_lds + kRecInfoOff + 4u * grp, i = rec_lds + kRecIdOff + 4u * grp;
   asm volatile(
       "ds_read_b64 %0, %3\n\t"
       "ds_read_b32 %1, %4\n\t"
       "ds_read_b32 %2, %5\n\t"
       "s_waitcnt lgkmcnt(0)"
-      : "=&v"(addr), "=&v"(len), "=&v"(id)
+      : "=&v"(addr), "=&v"(info), "=&v"(id)
       : "v"(a), "v"(l), "v"(i)
       : "memory");
 }
@@ -1371,23 +1376,34 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
     __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&recb[buf][wv][0], 4, 0, 0);
   };
   auto make_round = [&](uint64_t rnd, uint32_t buf) -> RaggedRound {
-    uint64_t sa;
-    uint32_t len, id;
-    read_record((uint32_t)(uintptr_t)(LdsVoid*)&recb[buf][wv][0], c.grp, sa, len, id);
-    const bool valid = rnd < total_rounds && rnd * kPacketsPerWave + c.grp < b.count;
-    if (!valid) {
-      sa = c.base4;
-      len = 0;
-    }
-    const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
-    const PacketGeo g = make_geo(sa, len + z);  // runs to the next 4-byte boundary
+    uint64_t ax;
+    uint32_t info, id;
+    read_record((uint32_t)(uintptr_t)(LdsVoid*)&recb[buf][wv][0], c.grp, ax, info, id);
+    // Everything per lane from the record's precomputed geometry (ragged_record); an
+    // invalid group (past the batch, or a re-read record) is an empty packet at base4.
+    const bool valid = rnd < total_rounds && ((ax >> kRecValidBit) & 1u);
+    const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
+    const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
+    const uint32_t pad = (info >> kRecPadShift) << 2;  // 128 nsteps - 4 nwords
+    const uint32_t v = valid ? (uint32_t)(ax >> kRecVShift) & 3u : 0u;
+    const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
     RaggedRound rr;
-    rr.ns = max(kDmaRing, wave_max_over_groups(g.nsteps));
-    rr.cb = g.a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
-    rr.top_slot = rr.ns - g.nsteps;
-    rr.direct = g.nsteps > 0 && chunk_kind(g, c.k, g.nsteps - 1, c.base4) == kChunkDirect;
-    uint64_t unused_tail;
-    rr.meta = round_meta(g, c.k, c.base4, valid, unused_tail, c.dummy) | (z << kMetaNTailShift);
+    rr.ns = max(kDmaRing, wave_max_over_groups(nsteps));
+    rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
+    rr.top_slot = rr.ns - nsteps;
+    // This lane's chunk at the top step, relative to top: chunk_offset(g, k, nsteps-1, top)
+    // = 4 nwords - 16 (k + 8 (nsteps - 1) + 1) = 112 - 16 k - pad.
+    const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
+    const bool inside = nsteps > 0 && rel > -16;  // not wholly before the packet
+    bool fb = false;                              // chunk_kind == kChunkFallback
+    if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
+      const uint64_t top = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
+      fb = top - c.base4 < (uint64_t)(-rel);
+    }
+    rr.direct = inside && !fb;
+    const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
+    rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
+              (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u);
     rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
     rr.id = id;
     // Fast: every packet starts at the same slot (same step count), no fallback chunk,
@@ -2344,7 +2360,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   if (err != hipSuccess) return err;
   Batch<true> b{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count};
   // Default: regions of the batch sorted by step class (region records kernel), then
-  // the round DMA kernel; =global: the whole batch sorted (histogram + records kernels).  ENET_CRC_RAGGED=flat: the flat-stream kernels (prep, main,
+  // the round DMA kernel.  ENET_CRC_RAGGED=flat: the flat-stream kernels (prep, main,
   // finish; the finish launch runs the streaming kernel's rounds for a batch the prep
   // kernel refused); =flatonly the same WITHOUT the fallback rounds (tests and A/B runs
   // on batches known to be in address order; any other batch leaves `out` undefined);
@@ -2357,7 +2373,6 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     if (v && strcmp(v, "groups") == 0) return 0;
     if (v && strcmp(v, "flat") == 0) return 3;
     if (v && strcmp(v, "flatonly") == 0) return 4;
-    if (v && strcmp(v, "global") == 0) return 5;
     return 1;
   }();
   if (count > 0xFFFFFFFFull || (ragged_mode != 0 && count < kSortMinPackets)) {
@@ -2372,7 +2387,6 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     hipLaunchKernelGGL(crc32_group_stream_kernel, dim3((unsigned)gblocks), dim3(kBlock), 0, stream, gb, out);
     return hipGetLastError();
   }
-  const bool stream_kernel = ragged_mode == 2;
   if (ragged_mode == 3 || ragged_mode == 4) {
     // Flat path: prep, main, finish (whose blocks run the streaming kernel's rounds
     // instead when the prep kernel refused the batch).  Regions = groups of the main
@@ -2430,14 +2444,14 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     const hipError_t ferr = hipFreeAsync(scratch, stream);
     return err != hipSuccess ? err : ferr;
   }
-  // ENET_CRC_RAGGED=global or =stream: the whole batch sorted by class.
+  // ENET_CRC_RAGGED=stream: the whole batch sorted by class (histogram + scatter), then
+  // the streaming kernel through the permutation.
   // >= 4096 packets per sort block: every records/scatter block reads the whole
   // histogram (16 x sort_blocks entries) to find its output positions.
   uint64_t sort_blocks = (count + 16 * kSortBlock - 1) / (16 * kSortBlock);
   sort_blocks = sort_blocks < 1024 ? sort_blocks : 1024;
   const size_t hist_bytes = ((size_t)kStepClasses * sort_blocks * 4 + 255) & ~(size_t)255;
-  const uint64_t rounds = (count + kPacketsPerWave - 1) / kPacketsPerWave;
-  const size_t tail_bytes = stream_kernel ? (size_t)count * 4 : (size_t)rounds * kRecordBytes;
+  const size_t tail_bytes = (size_t)count * 4;
   void* scratch = nullptr;
   hipMemPool_t pool = nullptr;
   err = scratch_pool(&pool);
@@ -2447,20 +2461,12 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   uint32_t* hist = static_cast<uint32_t*>(scratch);
   uint8_t* second = static_cast<uint8_t*>(scratch) + hist_bytes;
   hipLaunchKernelGGL(crc32_class_hist_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b, hist);
-  if (stream_kernel) {
-    uint32_t* perm = reinterpret_cast<uint32_t*>(second);
-    hipLaunchKernelGGL(crc32_class_scatter_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
-                       (const uint32_t*)hist, perm);
-    b.perm = perm;
-    Launcher<true> L{b, out, stream, blocks};
-    err = L.streaming();
-  } else {
-    hipLaunchKernelGGL(crc32_class_records_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
-                       (const uint32_t*)hist, second);
-    const RaggedDmaBatch rb{b.base, second, count, 0u, 0u};
-    hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
-    err = hipGetLastError();
-  }
+  uint32_t* perm = reinterpret_cast<uint32_t*>(second);
+  hipLaunchKernelGGL(crc32_class_scatter_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
+                     (const uint32_t*)hist, perm);
+  b.perm = perm;
+  Launcher<true> L{b, out, stream, blocks};
+  err = L.streaming();
   const hipError_t ferr = hipFreeAsync(scratch, stream);
   return err != hipSuccess ? err : ferr;
 }
