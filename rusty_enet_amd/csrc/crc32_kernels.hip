@@ -283,21 +283,16 @@ __device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_
 
 // The register of a packet the DMA kernels ran z = 0..3 zero bytes past its end (to the
 // next 4-byte boundary), from the tree value y: M8^-z M32 y = M8^m y with m = 4 - z, so
-// the last word's shift simply stops z bytes short.  With table t of the M32^1 set being
-// M8^(4-t) of one byte:  M8^m(y) = (y >> 8m) ^ sum_{j<m} table(4-m+j)[byte j of y].
-// One round of <= 4 independent lookups instead of M32 plus 2z dependent ones (the
-// inverse zero-byte steps through inv_top used before).  Call on lanes k == 0 only: copy = group, so the
-// 8 lanes of a wave never share a bank.
-__device__ __forceinline__ uint32_t finish_word(const uint32_t* lds, uint32_t y, uint32_t z) {
-  const uint32_t m = 4u - z, copy = (threadIdx.x >> 3) & 7u;
-  uint32_t r = m < 4u ? y >> (8u * m) : 0u;
-#pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
-    const uint32_t t = 4u - m + j;  // >= 4: byte j is shifted out entirely
-    const uint32_t v = lds[((y >> (8u * j)) & 0xFFu) * kRowDwords + kSetM1Bytes / 4 + (t & 3u) * kRepCopies + copy];
-    r ^= t < 4u ? v : 0u;
-  }
-  return r;
+// the last word's shift simply stops z bytes short.  Byte j of y reaches position 0
+// only if j < m, so
+//     M8^m(y) = M32(y << 8z) ^ (y >> (32 - 8z))      (second term 0 for z = 0):
+// the bytes that never reach the bottom leave unchanged, the others go through the
+// ordinary M32^1 lookups (one apply_rep: the lane's own conflict-free copies and
+// selectors, so it runs on every lane without masking; lane k == 0's value is used).
+__device__ __forceinline__ uint32_t finish_word(const uint32_t* lds, uint32_t y, uint32_t z, const Lookup& lk) {
+  const uint32_t lo = y << (8u * z);
+  const uint32_t hi = z ? y >> (32u - 8u * z) : 0u;
+  return apply_rep(lds, lo, hi, lk.lp1, lk);
 }
 
 // Sarwate byte steps (src/crc32.rs:43) over `ntail` bytes of `word` from byte `tsh`.
@@ -1051,8 +1046,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
       slot(ns - 1, false, true);
     }
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-    uint32_t reg = 0;
-    if (c.k == 0) reg = finish_word(lds, y, z);
+    uint32_t reg = finish_word(lds, y, z, c.lk);  // every lane; lane k == 0 holds the register
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     // Lane 8g+j keeps the checksum of group g in this wave's j-th round of 8; one store per 8.
     if (c.k == j) {
@@ -1170,8 +1164,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
       issue_order_fence();
     }
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-    uint32_t reg = 0;
-    if (c.k == 0) reg = finish_word(lds, y, z);
+    uint32_t reg = finish_word(lds, y, z, c.lk);  // every lane; lane k == 0 holds the register
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
       res = crc;
@@ -1446,8 +1439,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
       ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
     // Round end (record rnd[2] has landed: >= kDmaRing-1 DMAs since it was issued).
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-    uint32_t reg = 0;
-    if (c.k == 0) reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u);
+    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds the register
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
@@ -1698,8 +1690,7 @@ __global__ __launch_bounds__(kBlock) void crc32_group_stream_kernel(GsBatch batc
     const uint32_t col = lane >> 3;
     const uint32_t id = S.pmeta[wv][row][col][0], z = S.pmeta[wv][row][col][1];
     const uint32_t y = combine_tree(lds, hv.x, hv.y, hv.z, hv.w, c.lk);
-    uint32_t reg = 0;
-    if (k == 0) reg = finish_word(lds, y, z);
+    uint32_t reg = finish_word(lds, y, z, c.lk);  // lane k == 0 holds the register
     if (k == 0 && col < ncols) out[id] = __builtin_bswap32(~reg);
   };
 
@@ -2349,6 +2340,74 @@ static hipError_t scratch_pool(hipMemPool_t* out) {
   return hipSuccess;
 }
 
+// Round-record scratch of the default ragged path, kept per (device, stream) and reused
+// by the next launch on that stream (stream order makes the reuse safe), grown
+// stream-ordered when a batch needs more.  A hipMallocFromPoolAsync / hipFreeAsync pair
+// per launch left the GPU idle ~6 us between consecutive ragged launches (kernel
+// trace).  Up to kStreamScratchSlots streams are cached; launches on
+// further streams allocate per launch as before.  (A stream handle that is destroyed
+// and handed out again by HIP inherits its predecessor's buffer; a stream's pending
+// work completes before its handle can be reused, so the reuse stays ordered.)
+constexpr int kStreamScratchSlots = 64;
+struct StreamScratch {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+static std::mutex g_stream_scratch_lock;
+static StreamScratch g_stream_scratch[kStreamScratchSlots];
+
+// *owned = false: the buffer stays cached (do not free it after the launch).  Returns
+// with `held` locked: the caller launches the kernels that use the buffer before it
+// unlocks, so another thread on the same stream cannot free or regrow the buffer
+// ahead of those launches in stream order.
+static hipError_t records_scratch(hipStream_t stream, size_t need, hipMemPool_t pool, void** out, bool* owned,
+                                  std::unique_lock<std::mutex>& held) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const char* v = getenv("ENET_CRC_SCRATCH_CACHE");
+  const bool cache = !(v && strcmp(v, "0") == 0);
+  held = std::unique_lock<std::mutex>(g_stream_scratch_lock);
+  StreamScratch* slot = nullptr;
+  for (StreamScratch& s : g_stream_scratch) {
+    if (s.dev == dev && s.stream == stream) {
+      slot = &s;
+      break;
+    }
+    if (!slot && s.dev < 0) slot = &s;  // first free slot, unless the stream has one further on
+  }
+  if (!cache || !slot) {
+    *owned = true;
+    return hipMallocFromPoolAsync(out, need, pool, stream);
+  }
+  if (slot->dev == dev && slot->stream == stream && slot->bytes >= need) {
+    *owned = false;
+    *out = slot->ptr;
+    return hipSuccess;
+  }
+  if (slot->ptr) {
+    e = hipFreeAsync(slot->ptr, stream);  // same stream: after every earlier use
+    slot->ptr = nullptr;
+    slot->bytes = 0;
+    if (e != hipSuccess) return e;
+  }
+  const size_t grow = need + need / 4;
+  e = hipMallocFromPoolAsync(&slot->ptr, grow, pool, stream);
+  if (e != hipSuccess) {
+    slot->ptr = nullptr;
+    slot->dev = -1;
+    return e;
+  }
+  slot->dev = dev;
+  slot->stream = stream;
+  slot->bytes = grow;
+  *owned = false;
+  *out = slot->ptr;
+  return hipSuccess;
+}
+
 // Below this many packets the sort costs more than the padding it saves.
 constexpr uint64_t kSortMinPackets = 4096;
 
@@ -2432,7 +2491,9 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     hipMemPool_t pool = nullptr;
     err = scratch_pool(&pool);
     if (err != hipSuccess) return err;
-    err = hipMallocFromPoolAsync(&scratch, (size_t)rounds * kRecordBytes, pool, stream);
+    bool owned = true;
+    std::unique_lock<std::mutex> held;  // until both launches are enqueued
+    err = records_scratch(stream, (size_t)rounds * kRecordBytes, pool, &scratch, &owned, held);
     if (err != hipSuccess) return err;
     uint8_t* recs = static_cast<uint8_t*>(scratch);
     hipLaunchKernelGGL(crc32_region_records_kernel, dim3((unsigned)nregions), dim3(kRegionBlock), 0, stream, b,
@@ -2441,7 +2502,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     const RaggedDmaBatch rb{b.base, recs, count, xcd ? 1u : 0u, (ft && strcmp(ft, "0") == 0) ? 1u : 0u};
     hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
     err = hipGetLastError();
-    const hipError_t ferr = hipFreeAsync(scratch, stream);
+    const hipError_t ferr = owned ? hipFreeAsync(scratch, stream) : hipSuccess;
     return err != hipSuccess ? err : ferr;
   }
   // ENET_CRC_RAGGED=stream: the whole batch sorted by class (histogram + scatter), then

@@ -71,10 +71,10 @@ static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
       for (int k = 0; k + d < G; ++k) y[k] ^= t[k + d];
     }
     if (kExt) {
-      // finish_word: M8^m(y) = (y >> 8m) ^ sum_{j<m} op[0][4-m+j][byte j of y], m = 4 - z.
-      const uint32_t m = 4 - (uint32_t)z;
-      reg = m < 4 ? y[0] >> (8 * m) : 0u;
-      for (uint32_t j = 0; j < m; ++j) reg ^= T.op[0][4 - m + j][(y[0] >> (8 * j)) & 0xffu];
+      // finish_word: M8^(4-z)(y) = M32(y << 8z) ^ (y >> (32 - 8z)): the bytes shifted out
+      // of the register unchanged, the rest through the ordinary M32 tables.
+      const uint32_t zz = (uint32_t)z;
+      reg = op(0, zz ? y[0] << (8 * zz) : y[0]) ^ (zz ? y[0] >> (32 - 8 * zz) : 0u);
     } else {
       reg = op(0, y[0]);
     }

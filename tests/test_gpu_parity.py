@@ -268,3 +268,30 @@ def test_ragged_region_sort_edges(dev, count):
     offsets = (packed_offsets(lengths) + np.cumsum(gaps)).astype(np.uint64) + np.uint64(3)
     data = splitmix64_bytes(count + 1, int(offsets[-1] + lengths[-1]) + 8)
     assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
+
+
+# --- round-record scratch cached per stream (launch_ragged) ----------------------------------
+
+@pytest.mark.parametrize("cache", ["default", "0"])
+def test_ragged_scratch_per_stream(dev, cache, monkeypatch):
+    # Two streams, each launching sorted ragged batches that grow (the cached buffer is
+    # regrown stream-ordered) and shrink (reused), interleaved without synchronising in
+    # between; every result is kept and checked afterwards.  cache "0": allocate per launch.
+    if cache != "default":
+        monkeypatch.setenv("ENET_CRC_SCRATCH_CACHE", cache)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    jobs = []
+    for i, count in enumerate([5000, 40_000, 9000, 120_000, 4096, 70_000]):
+        lengths = ragged_lengths(ENET_SEED + 40 + i, count, lo=0, hi=1500)
+        offsets = packed_offsets(lengths) + np.uint64(i)
+        data = splitmix64_bytes(40 + i, int(lengths.sum()) + 16)
+        s = streams[i % 2]
+        with torch.cuda.stream(s):
+            d = to_dev(data, dev)
+            off = to_dev(offsets.astype(np.int64), dev)
+            ln = to_dev(lengths.astype(np.int32), dev)
+            out = rea.crc32_batch(d, offsets=off, lengths=ln, stream=s)
+        jobs.append((out, data, offsets, lengths, d, off, ln))
+    torch.cuda.synchronize()
+    for out, data, offsets, lengths, *_ in jobs:
+        assert np.array_equal(as_u32(out), _oracle.crc32_ragged(data, offsets, lengths))
