@@ -928,7 +928,14 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 // rounded up), the z = Lx - length bytes past its end are masked to zero in the last
 // word (lane 0's last slot), and the combine's last-word shift stops z bytes short
 // (finish_word).  No separate tail-word load.
-template <int NS>
+//
+// kNT: the DMAs carry the non-temporal hint.  Only for batches whose packets all END on
+// a 128-B line (launch_uniform): then every slot of a group is one whole aligned line,
+// never shared with a neighbour, and streaming whole lines past the caches is what the
+// memory system does fastest (tools/dma_probe PROBE_LINES: 8 aligned lines per
+// instruction with the kernel's lookups, 197 us non-temporal vs 219.5 us plain for
+// 1.26 GB; on lines a packet shares with its neighbour the hint costs a second fetch).
+template <int NS, bool kNT = false>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   constexpr int kDmaRing = kUniformRing;
   __shared__ __attribute__((aligned(16))) UniformDmaLds<kDmaRing> S;
@@ -980,7 +987,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   // LDS byte address of ring position 0 for this wave; DMA destinations are wave-uniform.
   const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
   auto dma = [&](uint64_t src, uint32_t q) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, kNT ? 2 : 0);
   };
 
   uint64_t rnd[kLook + 1];  // rnd[0]: current round; rnd[i]: i rounds ahead (wave-uniform)
@@ -2245,13 +2252,28 @@ static hipError_t launch_uniform_dma(const UniformBatch& u, uint32_t* out, hipSt
   return hipGetLastError();
 }
 
+// Long packets that all end on a 128-B line (e.g. 64 KiB buffers from an aligned base):
+// the runtime-step kernel with non-temporal DMAs.  ENET_CRC_NT=0 turns the hint off
+// (A/B runs).  Read per launch.
+static bool nt_lines(const UniformBatch& u) {
+  const char* v = getenv("ENET_CRC_NT");
+  if (v && strcmp(v, "0") == 0) return false;
+  const uint64_t lx = (u.length + 3u) & ~3u;
+  return ((u.base + lx) & 127u) == 0 && (u.stride & 127u) == 0;
+}
+
 // ns in 1..kMaxRoundSteps: the unrolled kernel; longer: the runtime-step kernel (NS = 0).
 template <int... I>
 static hipError_t dispatch_uniform_dma(int ns, const UniformBatch& u, uint32_t* out, hipStream_t stream,
                                        unsigned blocks, std::integer_sequence<int, I...>) {
   hipError_t e = hipErrorInvalidValue;
   const bool hit = ((ns == I + 1 ? (e = launch_uniform_dma<I + 1>(u, out, stream, blocks), true) : false) || ...);
-  return hit ? e : launch_uniform_dma<0>(u, out, stream, blocks);
+  if (hit) return e;
+  if (nt_lines(u)) {
+    hipLaunchKernelGGL((crc32_uniform_dma_kernel<0, true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+    return hipGetLastError();
+  }
+  return launch_uniform_dma<0>(u, out, stream, blocks);
 }
 
 // ns in 1..kMaxRoundSteps only (the register ring holds a whole round).

@@ -45,6 +45,10 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
     const uint64_t rr = wave + (r < nr ? r : nr - 1) * nwaves;  // global round index
     if (PAT == 0) return base + ((uint64_t)(rr * NS + s) % (npk * 1200 / 1024)) * 1024 + lane * 16;
     if (PAT == 3) return base + rr * 9600 + (uint64_t)s * 1024 + lane * 16;
+    // 1280-B packets (10 whole lines): 6 = 8 packets x one aligned line per slot (the
+    // 64-KiB kernel's shape), 8 = the same 10 KiB read as contiguous KiB.
+    if (PAT == 6) return base + (rr * 8 + g) * 1280 + (uint64_t)s * 128 + 16 * k;
+    if (PAT == 8) return base + rr * 10240 + (uint64_t)s * 1024 + lane * 16;
     if (PAT == 5) {  // 16 lanes per packet: slots 0-4 packets 0-3 of the round, slots 5-9 packets 4-7
       const uint64_t pk = rr * 8 + (s / 5) * 4 + lane / 16;
       int64_t off = -80 + 256 * (s % 5) + 16 * (int)(lane % 16);
@@ -154,6 +158,64 @@ __global__ __launch_bounds__(1024) void probe_regs(const uint8_t* __restrict__ b
   }
 }
 
+// Line-grid register ring (the shape of an absolute-line G1 kernel): round = 8
+// consecutive 1200-B packets, group g = packet; slot s of a lane reads the 16-B chunk
+// at line (last_line - 128 (NS-1 - s)) + 16 (7 - k); chunks outside the packet read a
+// zero chunk instead (no byte outside [S, E) is ever read).  NTM 0: plain loads, 1: all
+// nontemporal, 2: nontemporal except the first two and the last slot (the lines a packet
+// shares with its neighbours stay cacheable).
+__device__ __attribute__((aligned(64))) uint32_t g_probe_zero[16] = {0};
+template <int NSL, int NTM>
+__global__ __launch_bounds__(1024) void probe_lines(const uint8_t* __restrict__ buf, uint64_t npk, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[16384];
+  for (int i = threadIdx.x; i < 16384; i += 1024) tab[i] = i * 2654435761u;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const enet_crc::Lookup lk = enet_crc::make_lookup(lane);
+  const uint32_t g = lane / 8, k = lane % 8;
+  const uint64_t wave = (uint64_t)blockIdx.x * 16 + wv, nwaves = (uint64_t)gridDim.x * 16;
+  const uint64_t nrounds_total = npk / 8;
+  const uint64_t nr = wave < nrounds_total ? (nrounds_total - wave + nwaves - 1) / nwaves : 0;
+  const uint64_t base = (uint64_t)(uintptr_t)buf, zero = (uint64_t)(uintptr_t)g_probe_zero;
+  if (nr == 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  typedef __attribute__((address_space(1))) const u32x4a G4;
+  auto src = [&](uint64_t r, int s) -> G4* {
+    const uint64_t rr = wave + (r < nr ? r : nr - 1) * nwaves;
+    const uint64_t S = base + (rr * 8 + g) * 1200, E = S + 1200;
+    const uint64_t A = ((E - 1) & ~(uint64_t)127) - 128u * (NSL - 1 - s) + 16u * (7 - k);
+    return (G4*)(A < S || A >= E ? zero : A);
+  };
+  auto ld = [&](G4* a, int s) -> u32x4a {
+    const bool nt = NTM == 1 || (NTM == 2 && s >= 2 && s < NSL - 1);
+    return nt ? __builtin_nontemporal_load(a) : *a;
+  };
+  u32x4a q[NSL];
+#pragma unroll
+  for (int s = 0; s < NSL; ++s) { q[s] = ld(src(0, s), s); __builtin_amdgcn_sched_barrier(0); }
+  uint32_t h0 = lane, h1 = lane * 3, h2 = lane * 5, h3 = lane * 7;
+  auto step = [&](uint32_t h, uint32_t w) {
+    return tab[enet_crc::lookup_addr(h, lk.lp, lk, 0) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 1) / 4] ^
+           tab[enet_crc::lookup_addr(h, lk.lp, lk, 2) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 3) / 4] ^ w;
+  };
+  for (uint64_t r = 0; r < nr; ++r) {
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      const u32x4a v = q[s];
+      h0 = step(h0, v.x); h1 = step(h1, v.y); h2 = step(h2, v.z); h3 = step(h3, v.w);
+      __builtin_amdgcn_sched_barrier(0);
+      q[s] = ld(src(r + 1, s), s);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  out[blockIdx.x * 1024 + threadIdx.x] = h0 ^ h1 ^ h2 ^ h3;
+  if (threadIdx.x == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x] = t1 - t0;
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
 typedef void (*ProbeFn)(const uint8_t*, uint64_t, uint32_t*);
 static void run_fn(ProbeFn fn, const char* name, const uint8_t* d, uint64_t npk, uint32_t* out, int blocks);
 template <int PAT, int WORK, int NT, int R = 5>
@@ -198,6 +260,29 @@ int main() {
     free(h);
   }
   printf("CUs=%d, 1M x 1200 B, %s data\n", cus, getenv("PROBE_RANDOM") ? "random" : "0x5a");
+  if (getenv("PROBE_G1LINES")) {  // 1M x 1200 B, line grid, 11 slots
+    run_fn(probe_regs<0>, "P1 kernel lookups, register ring (current shape)", d, npk, out, cus);
+    run_fn(probe_regs<1>, "P1 kernel lookups, register ring nt", d, npk, out, cus);
+    run_fn(probe_lines<11, 0>, "line grid 11 slots, plain", d, npk, out, cus);
+    run_fn(probe_lines<11, 1>, "line grid 11 slots, nt", d, npk, out, cus);
+    run_fn(probe_lines<11, 2>, "line grid 11 slots, nt middle", d, npk, out, cus);
+    run_fn(probe_lines<11, 1>, "line grid 11 slots, nt (again)", d, npk, out, cus);
+    run_fn(probe_regs<0>, "P1 kernel lookups, register ring (again)", d, npk, out, cus);
+    return 0;
+  }
+  if (getenv("PROBE_LINES")) {  // 983,040 x 1280 B = same bytes as 1M x 1200 (GB/s column is exact)
+    const uint64_t n6 = npk * 1200 / 1280;
+    run<6, 0, 0, 5>("P6 aligned lines xor", d, n6, out, cus);
+    run<6, 0, 1, 5>("P6 aligned lines xor nt", d, n6, out, cus);
+    run<8, 0, 0, 5>("P8 contiguous xor", d, n6, out, cus);
+    run<8, 0, 1, 5>("P8 contiguous xor nt", d, n6, out, cus);
+    run<6, 2, 0, 5>("P6 aligned lines kernel lookups", d, n6, out, cus);
+    run<6, 2, 1, 5>("P6 aligned lines kernel lookups nt", d, n6, out, cus);
+    run<8, 2, 0, 5>("P8 contiguous kernel lookups", d, n6, out, cus);
+    run<8, 2, 1, 5>("P8 contiguous kernel lookups nt", d, n6, out, cus);
+    run<8, 2, 1, 4>("P8 contiguous kernel lookups nt R=4", d, n6, out, cus);
+    return 0;
+  }
   if (getenv("PROBE_REGS")) {
     run<1, 0, 0, 5>("P1 xor R=5", d, npk, out, cus);
     run<1, 2, 0, 5>("P1 kernel lookups, LDS-DMA R=5", d, npk, out, cus);
