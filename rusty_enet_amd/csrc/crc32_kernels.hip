@@ -1088,7 +1088,17 @@ struct UniformRegsLds {
   uint32_t next_dispatch;
 };
 
-template <int NS>
+//
+// kSplit (line-split loads): the ring has NS + 1 entries and each load reads, per group,
+// the chunks of ONE 128-B line (aligned to the packet end's 16-B residue) instead of one
+// end-aligned 128-B piece, which straddles two lines.  A piece i of the packet (end at
+// a1, j = (a1 mod 128) / 16) is the top 8 - j chunks of one line plus the bottom j of the
+// next, so lane k finds its slot-s chunk in entry s + lo, lo = (k < j): entry u holds
+// lane k's slot u - lo chunk (slots -1 and NS read the zero chunk).  Same bytes, same
+// lookups; one more load per round, but 8 whole lines per load instruction instead of
+// 16 partial ones (tools/dma_probe PROBE_SPLIT: 217-219 us vs 224-229 us for the piece
+// loads, same box, alternating).
+template <int NS, bool kSplit = false>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
@@ -1129,12 +1139,23 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 
   uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
   if (rnd0 >= total_rounds) return;
-  u32x4 q[NS];
+  constexpr int NE = kSplit ? NS + 1 : NS;  // ring entries
+  // Ring entry e of the round whose packet (this group's) starts at pb.
+  auto entry_src = [&](uint64_t pb, int e) -> uint64_t {
+    if constexpr (!kSplit) {
+      return slot_src(pb, e);
+    } else {
+      const uint32_t lo = c.k < ((uint32_t)(pb + lx) & 127u) >> 4 ? 1u : 0u;
+      const int32_t sl = e - (int32_t)lo;
+      return sl < 0 || sl >= NS ? c.dummy : slot_src(pb, sl);
+    }
+  };
+  u32x4 q[NE];
   {
     const uint64_t pb = packet_base(rnd0);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      q[s] = load_chunk(slot_src(pb, s));
+    for (int e = 0; e < NE; ++e) {
+      q[e] = load_chunk(entry_src(pb, e));
       issue_order_fence();
     }
   }
@@ -1144,10 +1165,13 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
     uint32_t d = 0;
     if (lane == 0) d = atomicAdd(&S.next_dispatch, 1u);
     const uint64_t pb = packet_base(rnd0), pbn = packet_base(rnd1);
+    const bool lo = kSplit && c.k < (((uint32_t)(pb + lx) & 127u) >> 4);
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      uint32_t w0 = q[s].x, w1 = q[s].y, w2 = q[s].z, w3 = q[s].w;
+      u32x4 v = q[s];
+      if constexpr (kSplit) v = lo ? q[s + 1] : q[s];
+      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
       if (s == 0) {
         const bool below = is_below(pb);
         if (__builtin_amdgcn_ballot_w64(below)) {
@@ -1167,7 +1191,11 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
         h3 = horner_main(lds, h3, w3, c.lk);
       }
       issue_order_fence();
-      q[s] = load_chunk(slot_src(pbn, s));  // the next round's slot s
+      q[s] = load_chunk(entry_src(pbn, s));  // the next round's entry s
+      issue_order_fence();
+    }
+    if constexpr (kSplit) {
+      q[NS] = load_chunk(entry_src(pbn, NS));
       issue_order_fence();
     }
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
@@ -2240,9 +2268,18 @@ static unsigned grid_for(uint64_t count, hipError_t& err) {
   return (unsigned)blocks;
 }
 
+// ENET_CRC_SPLIT=0: piece loads instead of line-split loads (A/B runs).  Read per launch.
+static bool use_split_loads() {
+  const char* v = getenv("ENET_CRC_SPLIT");
+  return !(v && strcmp(v, "0") == 0);
+}
+
 template <int NS>
 static hipError_t launch_uniform_regs(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
-  hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  if (use_split_loads())
+    hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS, true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  else
+    hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS, false>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
 

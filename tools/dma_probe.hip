@@ -216,6 +216,74 @@ __global__ __launch_bounds__(1024) void probe_lines(const uint8_t* __restrict__ 
   }
 }
 
+// End-aligned pieces from line-aligned loads: the 11 loads of a round each read ONE
+// whole 128-B line per group (lane k loads the chunk of that line it owns: piece t if
+// k >= j, piece t + 1 if k < j, j = (a1 mod 128) / 16), and slot s takes lane k's chunk
+// from ring entry s (k >= j) or s + 1 (k < j): 10 pieces, 9 lookup steps, as now, but no
+// line is split between two loads.  NTM 2: non-temporal except the two shared lines.
+template <int NTM>
+__global__ __launch_bounds__(1024) void probe_linesplit(const uint8_t* __restrict__ buf, uint64_t npk, uint32_t* __restrict__ out) {
+  constexpr int NSP = 10;
+  __shared__ __attribute__((aligned(16))) uint32_t tab[16384];
+  for (int i = threadIdx.x; i < 16384; i += 1024) tab[i] = i * 2654435761u;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const enet_crc::Lookup lk = enet_crc::make_lookup(lane);
+  const uint32_t g = lane / 8, k = lane % 8;
+  const uint64_t wave = (uint64_t)blockIdx.x * 16 + wv, nwaves = (uint64_t)gridDim.x * 16;
+  const uint64_t nrounds_total = npk / 8;
+  const uint64_t nr = wave < nrounds_total ? (nrounds_total - wave + nwaves - 1) / nwaves : 0;
+  const uint64_t base = (uint64_t)(uintptr_t)buf, zero = (uint64_t)(uintptr_t)g_probe_zero;
+  if (nr == 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  typedef __attribute__((address_space(1))) const u32x4a G4;
+  auto jj = [&](uint64_t r) -> uint32_t {
+    const uint64_t rr = wave + (r < nr ? r : nr - 1) * nwaves;
+    return (uint32_t)((base + (rr * 8 + g + 1) * 1200) & 127u) >> 4;
+  };
+  auto src = [&](uint64_t r, int u) -> G4* {  // ring entry u = line-load t = NSP - 1 - u
+    const uint64_t rr = wave + (r < nr ? r : nr - 1) * nwaves;
+    const uint64_t a1 = base + (rr * 8 + g + 1) * 1200;
+    const uint32_t j = (uint32_t)(a1 & 127u) >> 4;
+    const int pi = (NSP - 1 - u) + (k < j ? 1 : 0);
+    const bool real = pi >= 0 && pi < NSP && !(rr * 8 + g == 0 && pi == NSP - 1);
+    return (G4*)(real ? a1 - 128u * (uint64_t)pi - 16u * (k + 1) : zero);
+  };
+  auto ld = [&](G4* a, int u) -> u32x4a {
+    const bool nt = NTM == 1 || (NTM == 2 && u >= 1 && u < NSP);
+    return nt ? __builtin_nontemporal_load(a) : *a;
+  };
+  u32x4a q[NSP + 1];
+#pragma unroll
+  for (int u = 0; u <= NSP; ++u) { q[u] = ld(src(0, u), u); __builtin_amdgcn_sched_barrier(0); }
+  uint32_t h0 = lane, h1 = lane * 3, h2 = lane * 5, h3 = lane * 7;
+  auto step = [&](uint32_t h, uint32_t w) {
+    return tab[enet_crc::lookup_addr(h, lk.lp, lk, 0) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 1) / 4] ^
+           tab[enet_crc::lookup_addr(h, lk.lp, lk, 2) / 4] ^ tab[enet_crc::lookup_addr(h, lk.lp, lk, 3) / 4] ^ w;
+  };
+  uint32_t j = jj(0);
+  for (uint64_t r = 0; r < nr; ++r) {
+    const bool lo = k < j;
+#pragma unroll
+    for (int s = 0; s < NSP; ++s) {
+      const u32x4a v = lo ? q[s + 1] : q[s];
+      if (s == 0) { h0 = v.x; h1 = v.y; h2 = v.z; h3 = v.w; }
+      else { h0 = step(h0, v.x); h1 = step(h1, v.y); h2 = step(h2, v.z); h3 = step(h3, v.w); }
+      __builtin_amdgcn_sched_barrier(0);
+      q[s] = ld(src(r + 1, s), s);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    q[NSP] = ld(src(r + 1, NSP), NSP);
+    j = jj(r + 1);
+  }
+  out[blockIdx.x * 1024 + threadIdx.x] = h0 ^ h1 ^ h2 ^ h3;
+  if (threadIdx.x == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x] = t1 - t0;
+    reinterpret_cast<unsigned long long*>(out + (8 << 20))[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
 typedef void (*ProbeFn)(const uint8_t*, uint64_t, uint32_t*);
 static void run_fn(ProbeFn fn, const char* name, const uint8_t* d, uint64_t npk, uint32_t* out, int blocks);
 template <int PAT, int WORK, int NT, int R = 5>
@@ -260,6 +328,15 @@ int main() {
     free(h);
   }
   printf("CUs=%d, 1M x 1200 B, %s data\n", cus, getenv("PROBE_RANDOM") ? "random" : "0x5a");
+  if (getenv("PROBE_SPLIT")) {  // 1M x 1200 B: current shape vs line-split loads, alternating
+    for (int rep = 0; rep < 3; ++rep) {
+      run_fn(probe_regs<0>, "current shape (register ring)", d, npk, out, cus);
+      run_fn(probe_linesplit<2>, "line-split, nt except shared lines", d, npk, out, cus);
+      run_fn(probe_linesplit<0>, "line-split, plain", d, npk, out, cus);
+      run_fn(probe_linesplit<1>, "line-split, all nt", d, npk, out, cus);
+    }
+    return 0;
+  }
   if (getenv("PROBE_G1LINES")) {  // 1M x 1200 B, line grid, 11 slots
     run_fn(probe_regs<0>, "P1 kernel lookups, register ring (current shape)", d, npk, out, cus);
     run_fn(probe_regs<1>, "P1 kernel lookups, register ring nt", d, npk, out, cus);
