@@ -295,3 +295,38 @@ def test_ragged_scratch_per_stream(dev, cache, monkeypatch):
     torch.cuda.synchronize()
     for out, data, offsets, lengths, *_ in jobs:
         assert np.array_equal(as_u32(out), _oracle.crc32_ragged(data, offsets, lengths))
+
+
+# --- whole-line loads: line-split register ring, non-temporal long packets -----------------
+
+@pytest.mark.parametrize("split", ["default", "0"])
+@pytest.mark.parametrize("base_off", [0, 4, 12, 16, 48, 100, 124])
+def test_uniform_line_split_bases(dev, split, base_off, monkeypatch):
+    # Packet ends at every 16-B residue mod 128 (lo = 0..7 lanes taking entry s + 1),
+    # lengths that are and are not multiples of 16, the first packets within a chunk of
+    # the base (fallback loads), and a batch that ends exactly at the buffer's end.
+    if split != "default":
+        monkeypatch.setenv("ENET_CRC_SPLIT", split)
+    for stride, length, n in [(1200, 1200, 3001), (1392, 1392, 2999), (1204, 1200, 2048), (16, 16, 5000),
+                              (132, 128, 4000), (1796, 1792, 1500), (400, 396, 3333)]:
+        data = splitmix64_bytes(base_off * 7 + stride + length, base_off + (n - 1) * stride + length)
+        d = to_dev(data, dev)[base_off:]
+        got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
+        want = _oracle.crc32_uniform(data[base_off:], stride, length, n, threads=8)
+        assert np.array_equal(got, want), (stride, length, base_off)
+
+
+@pytest.mark.parametrize("nt", ["default", "0"])
+def test_long_packets_line_ends(dev, nt, monkeypatch):
+    # Non-temporal DMAs need every packet to end on a 128-B line: ends aligned with the
+    # starts aligned (64 KiB from an aligned base) or not (65536 - 128 from base + 128),
+    # and a base that breaks the line ends (the plain path).
+    if nt != "default":
+        monkeypatch.setenv("ENET_CRC_NT", nt)
+    for base_off, stride, length, n in [(0, 65536, 65536, 64), (128, 65536, 65408, 64), (4, 65536, 65536, 48),
+                                        (256, 8192, 4096, 300)]:
+        data = splitmix64_bytes(base_off + length, base_off + (n - 1) * stride + length)
+        d = to_dev(data, dev)[base_off:]
+        got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
+        want = _oracle.crc32_uniform(data[base_off:], stride, length, n, threads=8)
+        assert np.array_equal(got, want), (base_off, stride, length)
