@@ -39,6 +39,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="", help="run only the cases whose name contains this")
+    ap.add_argument("--lengths", default="", help="comma list: ragged-equal cases at these lengths only")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n = 1 << 20
@@ -54,11 +55,19 @@ def main() -> int:
         ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
         return (lambda: rea.crc32_batch(data, offsets=off, lengths=ln, out=out)), int(lengths.sum())
 
-    for length in (1200, 1392, 640):
+    if args.lengths:
+        for length in (int(x) for x in args.lengths.split(",")):
+            fn, nb = ragged(np.full(n, length, dtype=np.uint32))
+            cases.append((f"ragged-equal {length}", fn, nb))
+    for length in (() if args.lengths else (1200, 1392, 640)):
         cases.append((f"uniform {length}", uniform(length), n * length))
         fn, nb = ragged(np.full(n, length, dtype=np.uint32))
         cases.append((f"ragged-equal {length}", fn, nb))
     g2 = ragged_lengths(ENET_SEED, n, lo=64, hi=1392)
+    if args.lengths:
+        g16 = (g2 + 15) // 16 * 16
+        fn, nb = ragged(g16)
+        cases.append(("ragged G2 lengths rounded to 16", fn, nb))
     fn, nb = ragged(g2)
     cases.append(("ragged G2 U[64,1392]", fn, nb))
     fn, nb = ragged(np.sort(g2))
