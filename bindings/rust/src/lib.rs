@@ -74,6 +74,7 @@ extern "C" {
                                            d_slot_offsets: *const u32, d_slot_values: *const u32, count: u64,
                                            d_crc: *mut u32, hip_stream: *mut c_void) -> c_int;
     pub fn enet_crc32_slot_adjust(crc: u32, old_slot: u32, new_slot: u32, bytes_after_slot: u32) -> u32;
+    pub fn enet_crc32_combine(crc_a: u32, crc_b: u32, len_b: u64) -> u32;
 
     // include/enet_range_amd.h
     pub fn enet_range_scratch_bytes(workers: u64) -> u64;
@@ -111,6 +112,12 @@ fn last_error(status: c_int) -> CrcError {
 /// when it processes the datagram (rusty_enet src/c/protocol.rs:1483-1499).
 pub fn slot_adjust(crc: u32, old_slot: u32, new_slot: u32, bytes_after_slot: u32) -> u32 {
     unsafe { enet_crc32_slot_adjust(crc, old_slot, new_slot, bytes_after_slot) }
+}
+
+/// `crc32(&[a, b])` from `crc32(&[a])`, `crc32(&[b])` and `b.len()`: the merged digest of
+/// shards checksummed on different GPUs (host arithmetic, no device work).
+pub fn combine(crc_a: u32, crc_b: u32, len_b: u64) -> u32 {
+    unsafe { enet_crc32_combine(crc_a, crc_b, len_b) }
 }
 
 #[derive(Debug, Clone, Copy, PartialEq, Eq)]

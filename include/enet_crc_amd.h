@@ -213,6 +213,17 @@ ENET_CRC_API uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, ui
                                              uint32_t bytes_after_slot);
 
 /*
+ * Host-side merge (no device work; O(log len_b) GF(2) operator squarings).  Given the
+ * checksums crc_a = crc32(&[a]) and crc_b = crc32(&[b]) in the reference's convention
+ * (src/crc32.rs:46, bswap32(~reg)), returns crc32(&[a, b]), the checksum of the
+ * concatenation, where len_b is the byte length of b (any u64).  This is the merged
+ * digest of a sharded batch: per-shard or per-packet checksums
+ * computed on different GPUs combine on the host without touching the bytes again.
+ * len_b == 0 returns crc_a.
+ */
+ENET_CRC_API uint32_t enet_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/*
  * Pinned receive ring.  The host path above copies pageable
  * buffers into pinned staging first; a ring lets the receive loop put datagrams
  * straight into pinned memory (e.g. recvmmsg into slot memory, the role of

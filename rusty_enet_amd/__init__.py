@@ -10,6 +10,7 @@ from .checksum import (  # noqa: F401
     checksum_fn,
     crc32,
     crc32_batch,
+    crc32_combine,
     crc32_ragged_device,
     crc32_shards_device,
     crc32_uniform_device,
@@ -23,7 +24,7 @@ from .checksum import (  # noqa: F401
 from .range_coder import RangeCoder, compress_batch, decompress_batch, gather_slices  # noqa: F401
 
 __all__ = [
-    "Context", "CrcError", "NativeLibraryMissing", "checksum_fn", "crc32", "crc32_batch",
+    "Context", "CrcError", "NativeLibraryMissing", "checksum_fn", "crc32", "crc32_batch", "crc32_combine",
     "crc32_ragged_device", "crc32_shards_device", "crc32_uniform_device", "shard_bounds_native", "default_context", "insert_batch", "slot_adjust",
     "verify_batch", "RangeCoder", "compress_batch", "decompress_batch", "gather_slices",
 ]

@@ -82,6 +82,7 @@ _SIGNATURES = {
                                         [ctypes.c_void_p] * 2),
     "enet_crc32_slot_adjust": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_uint32]),
+    "enet_crc32_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     "enet_crc_ring_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.POINTER(ctypes.c_void_p)]),
     "enet_crc_ring_destroy": (None, [ctypes.c_void_p]),

@@ -342,6 +342,17 @@ def slot_adjust(crc: int, old_slot: int, new_slot: int, bytes_after_slot: int) -
                                         int(bytes_after_slot))
 
 
+def crc32_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """``crc32(&[a, b])`` from ``crc32(&[a])``, ``crc32(&[b])`` and ``len(b)``.
+
+    Host-side merge (``enet_crc32_combine``): the merged digest of shards checksummed
+    on different GPUs, without touching the bytes again.
+    """
+    if len_b < 0:
+        raise ValueError("len_b must be >= 0")
+    return lib().enet_crc32_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, int(len_b))
+
+
 def _slot_batch_args(data, offsets, lengths, slot_offsets, slot_values):
     import torch
 

@@ -662,6 +662,34 @@ uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, uint32_t new_sl
   return crc ^ slot_delta(l, kSlotLevels, l, old_slot ^ new_slot, bytes_after_slot);
 }
 
+// reg(a || b) = M8^n(reg(a) ^ 0xFFFFFFFF) ^ reg(b) with n = |b| (the initial register's
+// share of reg(b) is M8^n(0xFFFFFFFF)), and reg = ~bswap32(checksum), so
+//   checksum(a || b) = bswap32(M8^n(bswap32(crc_a))) ^ crc_b.
+// M8^n by binary powering of M8 as a 32 x 32 GF(2) matrix (column i = M8(1 << i)).
+uint32_t enet_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+  if (len_b == 0) return crc_a;
+  auto apply = [](const uint32_t* m, uint32_t x) {
+    uint32_t r = 0;
+    for (int i = 0; x != 0; ++i, x >>= 1)
+      if (x & 1u) r ^= m[i];
+    return r;
+  };
+  uint32_t op[32], sq[32];
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t x = 1u << i;
+    op[i] = (x >> 8) ^ kOpTables.sarwate[x & 0xffu];  // M8, src/crc32.rs:43 with a zero byte
+  }
+  uint32_t v = __builtin_bswap32(crc_a);
+  for (uint64_t n = len_b;;) {
+    if (n & 1u) v = apply(op, v);
+    n >>= 1;
+    if (n == 0) break;
+    for (int i = 0; i < 32; ++i) sq[i] = apply(op, op[i]);
+    for (int i = 0; i < 32; ++i) op[i] = sq[i];
+  }
+  return __builtin_bswap32(v) ^ crc_b;
+}
+
 int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, uint32_t* out_crc) {
   if (!ctx || !out_crc || (nbufs > 0 && !bufs)) return ENET_CRC_E_INVALID;
   size_t total = 0;

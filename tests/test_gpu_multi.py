@@ -100,6 +100,12 @@ def test_shards_device_two_shards(dev):
     torch.cuda.synchronize()
     assert np.array_equal(oa.cpu().numpy().view(np.uint32), _oracle.crc32_uniform(a, L, L, n, threads=8))
     assert np.array_equal(ob.cpu().numpy().view(np.uint32), _oracle.crc32_ragged(b, offsets, lengths))
+    # Merged digest of shard a: its packets are back to back, so the
+    # GPU's per-packet checksums fold (enet_crc32_combine) into the checksum of its bytes.
+    digest = None
+    for c in oa.cpu().numpy().view(np.uint32).tolist():
+        digest = c if digest is None else rea.crc32_combine(digest, c, L)
+    assert digest == _oracle.crc32([a])
 
 
 @pytest.mark.parametrize("mode", [_native.ENET_CRC_PERCALL_COPY, _native.ENET_CRC_PERCALL_ZEROCOPY,

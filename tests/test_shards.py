@@ -14,6 +14,8 @@ import torch.multiprocessing as mp
 
 import _oracle
 from _data import ENET_SEED, packed_offsets, ragged_lengths, splitmix64_bytes
+import torch
+from rusty_enet_amd import crc32_combine
 from rusty_enet_amd.shards import max_over_ranks, shard_bounds
 
 
@@ -68,6 +70,21 @@ def _rank_main(rank, world, port, n, result_dir):
         end = int(off[hi - 1] + ln[hi - 1]) if hi > lo else 0
         out = _oracle.crc32_ragged(data[base:end], off[lo:hi] - np.uint64(base), ln[lo:hi])
         np.save(os.path.join(result_dir, f"rank{rank}.npy"), out)
+        # Merged digest: the shard's packets fold into the digest of its
+        # bytes (packed: the concatenation), then the (crc, bytes) pairs of the ranks
+        # fold on rank 0 -- 16 B per rank, host arithmetic (enet_crc32_combine).
+        digest = None
+        for c, L in zip(out.tolist(), ln[lo:hi].tolist()):
+            digest = c if digest is None else crc32_combine(digest, c, L)
+        pair = torch.tensor([-1 if digest is None else digest, end - base], dtype=torch.int64)
+        pairs = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(pairs, pair)
+        if rank == 0:
+            merged = None
+            for c, nbytes in (p.tolist() for p in pairs):
+                if c >= 0:
+                    merged = c if merged is None else crc32_combine(merged, c, nbytes)
+            np.save(os.path.join(result_dir, "merged.npy"), np.array([merged], dtype=np.uint64))
         t = max_over_ranks([float(rank + 1), -float(rank)])
         assert t == [float(world), 0.0], t
     finally:
@@ -83,3 +100,4 @@ def test_gloo_world2_shards_cover_batch(tmp_path):
     data = splitmix64_bytes(ENET_SEED + 1, int(ln.sum()))
     want = _oracle.crc32_ragged(data, packed_offsets(ln), ln)
     assert np.array_equal(got, want)
+    assert int(np.load(tmp_path / "merged.npy")[0]) == _oracle.crc32([data])
