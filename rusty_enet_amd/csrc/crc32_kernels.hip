@@ -1076,6 +1076,172 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
 }
 
 // ---------------------------------------------------------------------------------
+// Wave-per-packet kernel for long uniform packets (the default from 4 KiB): the whole wave
+// works on ONE packet and each step is one KiB of it, lane l taking the 16-B chunk
+// at a1 - 16 (l + 1) - 1024 (ns - 1 - s).  So every DMA instruction reads 1 KiB of
+// contiguous bytes (8 consecutive 128-B lines) instead of one line from each of 8
+// packets, the shape the read probes stream fastest with the non-temporal hint
+// (tools/dma_probe: whole contiguous KiB 193-199 us for 1.26 GB).
+// Arithmetic: the same 4 word streams per lane, with the Horner operator M32^256 (a
+// 1-KiB stride) in the replicated block's main set; at the packet's end the in-lane
+// M32^1 combine, then a 6-level tree over the 64 lanes (M32^4 .. M32^128; DPP inside
+// 16-lane rows, shuffles for the last two levels) and finish_word on lane 0.
+// Same LDS-DMA ring, waits, head/tail masking and dispatch as crc32_uniform_dma_kernel
+// (a "round" is one packet here).  Packets of >= kWaveRing KiB only.
+// ---------------------------------------------------------------------------------
+constexpr int kWaveRing = 4;
+constexpr uint32_t kWaveStep = 1024;
+constexpr int kWaveTreeLevels = 6;
+constexpr uint32_t kWaveTreeDword = kRepDwords;
+constexpr uint32_t kWaveLdsDwords = kWaveTreeDword + kWaveTreeLevels * 1024;
+static_assert(kMainLevel + 3 < kOpLevels, "M32^256 table level");
+
+struct WaveDmaLds {
+  uint32_t tables[kWaveLdsDwords];
+  u32x4 ring[kWaveRing][kWavesPerBlock][64];
+  uint32_t next_dispatch;
+};
+static_assert(sizeof(WaveDmaLds) <= 160 * 1024, "LDS");
+
+__device__ __forceinline__ void fill_lds_wave(uint32_t* lds) {
+  const int t = threadIdx.x;  // (table, entry) pairs: 4 x 256 = kBlock
+  {
+    const int tab = t >> 8, i = t & 255;
+    const uint32_t v = g_op_tables.op[kMainLevel + 3][tab][i], v1 = g_op_tables.op[0][tab][i];
+    const u32x4 vv = {v, v, v, v}, vv1 = {v1, v1, v1, v1};
+    u32x4* dst = reinterpret_cast<u32x4*>(lds + i * kRowDwords + tab * kRepCopies);
+    u32x4* dst1 = reinterpret_cast<u32x4*>(lds + i * kRowDwords + kSetM1Bytes / 4 + tab * kRepCopies);
+    dst[0] = vv;
+    dst[1] = vv;
+    dst1[0] = vv1;
+    dst1[1] = vv1;
+  }
+  for (int x = t; x < kWaveTreeLevels * 1024; x += kBlock) {
+    const int set = x >> 10, rem = x & 1023;  // set l: M32^(4 * 2^l)
+    lds[kWaveTreeDword + x] = g_op_tables.op[set + 2][rem >> 8][rem & 255];
+  }
+}
+
+// The packet's register before the shift of its last word (register = M32 y), valid
+// on lane 0: in-lane Horner over the 4 word slots, then lane l + d folds into lane l
+// through M32^(4d) for d = 1, 2, 4, ..., 32.
+__device__ __forceinline__ uint32_t combine_wave(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
+                                                uint32_t h3, const Lookup& lk) {
+  uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
+  y = apply_rep(lds, y, h2, lk.lp1, lk);
+  y = apply_rep(lds, y, h3, lk.lp1, lk);
+  const uint32_t l = threadIdx.x & 63u;
+  const uint32_t* tree = lds + kWaveTreeDword;
+  uint32_t t = 0;
+  if (l & 1u) t = apply_small(tree, y);
+  y ^= from_lane_plus<1>(t);
+  if ((l & 3u) == 2u) t = apply_small(tree + 1024, y);
+  y ^= from_lane_plus<2>(t);
+  if ((l & 7u) == 4u) t = apply_small(tree + 2048, y);
+  y ^= from_lane_plus<4>(t);
+  if ((l & 15u) == 8u) t = apply_small(tree + 3072, y);
+  y ^= from_lane_plus<8>(t);
+  if ((l & 31u) == 16u) t = apply_small(tree + 4096, y);
+  y ^= (uint32_t)__shfl((int)t, (int)((l + 16u) & 63u), 64);
+  if (l == 32u) t = apply_small(tree + 5120, y);
+  y ^= (uint32_t)__shfl((int)t, (int)((l + 32u) & 63u), 64);
+  return y;
+}
+
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void crc32_wave_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  constexpr int kDmaRing = kWaveRing;
+  __shared__ __attribute__((aligned(16))) WaveDmaLds S;
+  uint32_t* const lds = S.tables;
+  auto& ring = S.ring;
+  uint32_t& next_dispatch = S.next_dispatch;
+  constexpr int kLook = 2;
+  if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
+  fill_lds_wave(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(u.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t total = u.count;
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto round_of = [&](uint32_t d) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
+  const uint32_t lx = (u.length + 3u) & ~3u, z = lx - u.length;
+  const int32_t ns = (int32_t)((lx + kWaveStep - 1) / kWaveStep);  // >= kDmaRing (launch_uniform)
+  const uint32_t last_mask = lane == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+  // This lane's step-0 chunk relative to its packet's start (> -1024).
+  const int64_t rel0 = (int64_t)lx - 16 * (int64_t)(lane + 1u) - (int64_t)kWaveStep * (ns - 1);
+  uint32_t am[4], xm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    am[j] = rel0 + 4 * j >= 0 ? 0xFFFFFFFFu : 0u;
+    xm[j] = rel0 + 4 * j == 0 ? kInitRegister : 0u;
+  }
+  const bool none0 = rel0 <= -16;
+  const bool part0 = rel0 < 0 && rel0 > -16;
+  const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;
+  auto packet_base = [&](uint64_t p) -> uint64_t { return u.base + (p < total ? p : total - 1) * u.stride; };
+  auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
+  auto slot_src = [&](uint64_t pb, int32_t s) -> uint64_t {
+    if (s != 0) return pb + (uint64_t)(rel0 + (int64_t)kWaveStep * s);
+    return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
+  };
+  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
+  auto dma = [&](uint64_t src, uint32_t q) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, kNT ? 2 : 0);
+  };
+
+  uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
+  if (rnd0 >= total) return;
+  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
+#pragma unroll
+  for (int f = 0; f < kDmaRing; ++f) dma(slot_src(packet_base(rnd0), f), (uint32_t)f);
+  uint32_t q = 0;
+  u32x4 nextv = read_landed_slot<kDmaRing - 1>(ring0 + lane * 16u);
+  while (rnd0 < total) {
+    uint32_t d = 0;
+    if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
+    const uint64_t pb = packet_base(rnd0), pb_next = packet_base(rnd1);
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    auto slot = [&](int32_t s, bool top, bool last) {
+      const u32x4 v = nextv;
+      const int32_t f = s + kDmaRing;
+      dma(f < ns ? slot_src(pb, f) : slot_src(pb_next, f - ns), q);
+      q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
+      const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
+      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+      if (top) {
+        const bool below = is_below(pb);
+        if (__builtin_amdgcn_ballot_w64(below)) {
+          if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
+        }
+      }
+      if (last) w3 &= last_mask;
+      if (top) {
+        h0 = (w0 & am[0]) ^ xm[0];
+        h1 = (w1 & am[1]) ^ xm[1];
+        h2 = (w2 & am[2]) ^ xm[2];
+        h3 = (w3 & am[3]) ^ xm[3];
+        nextv = read_landed_slot<kDmaRing - 1>(next_addr);
+      } else {
+        horner_step_and_read<kDmaRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, nextv);
+      }
+      issue_order_fence();
+    };
+    slot(0, true, false);  // ns >= kDmaRing > 1
+    for (int32_t s = 1; s < ns - 1; ++s) slot(s, false, false);
+    slot(ns - 1, false, true);
+    const uint32_t y = combine_wave(lds, h0, h1, h2, h3, c.lk);
+    const uint32_t reg = finish_word(lds, y, z, c.lk);  // lane 0 holds the register
+    if (lane == 0) out[rnd0] = __builtin_bswap32(~reg);
+    rnd0 = rnd1;
+    rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+// ---------------------------------------------------------------------------------
 // Uniform kernel, register form (ENET_CRC_UNIFORM=regs).  Same geometry, arithmetic,
 // dispatch, result batching and trailing-byte handling as crc32_uniform_dma_kernel,
 // but the packet bytes go straight to VGPRs: the next round's NS chunks are loaded
@@ -2344,6 +2510,20 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
     UniformBatch u{b0, stride, length, count};
     const char* xv = getenv("ENET_CRC_XCD");
     u.xcd_swizzle = (xv && strcmp(xv, "1") == 0) ? 1u : 0u;
+    // Packets of >= 4 KiB: the wave-per-packet kernel (1-KiB contiguous loads); 64-KiB
+    // buffers 338-346 us vs 371-374 us for the 8-packets-per-wave DMA kernel, 3 alternating
+    // pairs.  ENET_CRC_LONG=group restores the latter (A/B runs).
+    const char* lv = getenv("ENET_CRC_LONG");
+    if (!(lv && strcmp(lv, "group") == 0) && length >= (uint32_t)kWaveRing * kWaveStep) {
+      uint64_t wblocks = (count + kWavesPerBlock - 1) / kWavesPerBlock;
+      const int cus = cu_count_for_current_device();
+      if (wblocks > (uint64_t)cus) wblocks = (uint64_t)cus;
+      if (nt_lines(u))
+        hipLaunchKernelGGL((crc32_wave_dma_kernel<true>), dim3((unsigned)wblocks), dim3(kBlock), 0, stream, u, out);
+      else
+        hipLaunchKernelGGL((crc32_wave_dma_kernel<false>), dim3((unsigned)wblocks), dim3(kBlock), 0, stream, u, out);
+      return hipGetLastError();
+    }
     if (use_regs_uniform() && nsx <= kMaxRoundSteps)
       return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
     return dispatch_uniform_dma(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});

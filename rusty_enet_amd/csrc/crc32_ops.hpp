@@ -28,7 +28,7 @@ namespace enet_crc {
 
 constexpr uint32_t kReflectedPoly = 0xEDB88320u;
 constexpr uint32_t kInitRegister = 0xFFFFFFFFu;
-constexpr int kOpLevels = 8;  // M32^1 .. M32^128
+constexpr int kOpLevels = 9;  // M32^1 .. M32^256
 
 struct OpTables {
   uint32_t sarwate[256];

@@ -330,3 +330,37 @@ def test_long_packets_line_ends(dev, nt, monkeypatch):
         got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
         want = _oracle.crc32_uniform(data[base_off:], stride, length, n, threads=8)
         assert np.array_equal(got, want), (base_off, stride, length)
+
+
+@pytest.mark.parametrize("long_mode", ["default", "group"])
+@pytest.mark.parametrize("base_off", [0, 4, 12, 128, 1000])
+def test_long_packets_wave_kernel(dev, long_mode, base_off, monkeypatch):
+    # Default: one wave per packet, 1-KiB steps (crc32_wave_dma_kernel); ENET_CRC_LONG=group:
+    # 8 packets per wave (crc32_uniform_dma_kernel<0>).
+    # Lengths from the 4-KiB minimum up, multiples of 1 KiB and 128 B or not, odd lengths
+    # (bytes past the end masked), gaps between packets, packets within a chunk of the
+    # base (fallback loads), counts that are not multiples of the wave count.
+    if long_mode != "default":
+        monkeypatch.setenv("ENET_CRC_LONG", long_mode)
+    for stride, length, n in [(65536, 65536, 200), (4096, 4096, 3001), (4100, 4097, 999), (5000, 4999, 777),
+                              (12288, 10001, 300), (65540, 65537, 33), (70000, 65536, 17), (8192, 8191, 1),
+                              (4096, 4096, 4097)]:
+        data = splitmix64_bytes(base_off * 3 + stride + length, base_off + (n - 1) * stride + length)
+        d = to_dev(data, dev)[base_off:]
+        got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
+        want = _oracle.crc32_uniform(data[base_off:], stride, length, n, threads=8)
+        assert np.array_equal(got, want), (long_mode, stride, length, n, base_off)
+
+
+def test_full_shard_large_group_kernel(dev, monkeypatch):
+    # The G4 per-GPU shard (32,768 x 64 KiB) through the 8-packets-per-wave kernel
+    # (ENET_CRC_LONG=group; the default path is test_full_shard_large_32768_x_64k).
+    monkeypatch.setenv("ENET_CRC_LONG", "group")
+    n, L = 32768, 65536
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED + 5)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    got = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
+    want = _oracle.crc32_uniform(d.cpu().numpy(), L, L, n, threads=16)
+    del d
+    assert np.array_equal(got, want)
