@@ -495,9 +495,16 @@ def shard_2m(dev, rank: int, steps: int, warmup: int, barrier) -> dict:
 
 def uniform_point(dev, rank: int, n: int, L: int, steps: int, warmup: int, barrier) -> dict:
     """n x L-byte uniform packets timed on this GPU (verified on a sample first)."""
+    return config_point("uniform", dev, rank, n, steps, warmup, barrier, length=L)
+
+
+def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, barrier,
+                 length: int | None = None) -> dict:
+    """One more workload timed on this GPU after the main line (verified on a sample first):
+    the N = 1 line carries the other BASELINE configs' per-GPU shapes next to G1."""
     import torch
 
-    step, nbytes, _, out, spec = make_workload("uniform", rank, n, dev, length=L)
+    step, nbytes, _, out, spec = make_workload(name, rank, n, dev, length=length)
     step()
     torch.cuda.synchronize()
     verify_sample(out, spec)
@@ -585,6 +592,12 @@ def main(argv=None) -> int:
         # The reference's default MTU (src/consts.rs:32; SURVEY.md 8(a) note): 1M x 1392 B.
         extra["mtu_1392"] = uniform_point(dev, rank, CONFIGS["uniform"][1], 1392, min(args.steps, 100), args.warmup,
                                           barrier)
+        # BASELINE configs[2] (G2, ragged) and the per-GPU shard of configs[4] (G4, 32,768 x
+        # 64 KiB): the same measurement as `--config ragged` / `--config large`.
+        extra["ragged_g2"] = config_point("ragged", dev, rank, CONFIGS["ragged"][1], min(args.steps, 100),
+                                          args.warmup, barrier)
+        extra["large_64k"] = config_point("large", dev, rank, CONFIGS["large"][1], min(args.steps, 50),
+                                          args.warmup, barrier)
 
     if rank == 0:
         total_bytes = nbytes * world
