@@ -92,12 +92,20 @@ def test_shards_device_two_shards(dev):
     oa = torch.empty(n, dtype=torch.int32, device=dev)
     ob = torch.empty(lengths.size, dtype=torch.int32, device=dev)
     s2 = torch.cuda.Stream(device=dev)
+    # A third shard of 64-KiB buffers (the wave-per-packet kernel) on a stream of its own.
+    nc, LC = 96, 65536
+    cb = splitmix64_bytes(30, nc * LC)
+    dc = torch.from_numpy(cb).to(dev)
+    oc = torch.empty(nc, dtype=torch.int32, device=dev)
+    s3 = torch.cuda.Stream(device=dev)
     rea.crc32_shards_device([
         {"data": da, "stride": L, "length": L, "count": n, "out": oa},
         {"data": db, "offsets": torch.from_numpy(offsets.astype(np.int64)).to(dev),
          "lengths": torch.from_numpy(lengths.astype(np.int32)).to(dev), "out": ob, "stream": s2},
+        {"data": dc, "stride": LC, "length": LC, "count": nc, "out": oc, "stream": s3},
     ])
     torch.cuda.synchronize()
+    assert np.array_equal(oc.cpu().numpy().view(np.uint32), _oracle.crc32_uniform(cb, LC, LC, nc, threads=8))
     assert np.array_equal(oa.cpu().numpy().view(np.uint32), _oracle.crc32_uniform(a, L, L, n, threads=8))
     assert np.array_equal(ob.cpu().numpy().view(np.uint32), _oracle.crc32_ragged(b, offsets, lengths))
     # Merged digest of shard a: its packets are back to back, so the
