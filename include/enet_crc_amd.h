@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ENET_CRC_ABI_VERSION 3
+#define ENET_CRC_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define ENET_CRC_API __attribute__((visibility("default")))
@@ -71,6 +71,7 @@ typedef struct enet_crc_ctx enet_crc_ctx;
  * entry points stop it first.  Datagrams above 4096 B take the zero-copy path. */
 #define ENET_CRC_PERCALL_PERSISTENT 2
 
+/* ENET_CRC_ABI_VERSION: 4 added enet_crc32_combine; nothing was removed or changed. */
 ENET_CRC_API int enet_crc_abi_version(void);
 ENET_CRC_API const char* enet_crc_strerror(int status);
 /* hipError_t of the last failing HIP call made by this thread (0 if none). */

@@ -117,7 +117,7 @@ ENET_CRC_PERCALL_COPY = 0
 ENET_CRC_PERCALL_ZEROCOPY = 1
 ENET_CRC_PERCALL_PERSISTENT = 2
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 def lib() -> ctypes.CDLL:
