@@ -364,3 +364,22 @@ def test_full_shard_large_group_kernel(dev, monkeypatch):
     want = _oracle.crc32_uniform(d.cpu().numpy(), L, L, n, threads=16)
     del d
     assert np.array_equal(got, want)
+
+
+def test_long_packets_random_layouts(dev):
+    # 60 random uniform layouts through the default path for long packets (the
+    # wave-per-packet kernel from 4 KiB, the 8-packets-per-wave DMA kernel below it):
+    # lengths 1.5-70 KB, strides >= length (4-B multiples: the aligned path), base offsets
+    # 0-1020, counts 1-300.
+    rng = np.random.default_rng(2026)
+    for case in range(60):
+        length = int(rng.integers(1500, 70_000))
+        stride = length + 4 * int(rng.integers(0, 64)) if case % 3 else length
+        stride = (stride + 3) & ~3
+        base_off = 4 * int(rng.integers(0, 256))
+        n = int(rng.integers(1, 300))
+        data = splitmix64_bytes(case + 1, base_off + (n - 1) * stride + length)
+        d = to_dev(data, dev)[base_off:]
+        got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
+        want = _oracle.crc32_uniform(data[base_off:], stride, length, n, threads=8)
+        assert np.array_equal(got, want), (case, stride, length, n, base_off)
