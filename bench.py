@@ -121,7 +121,14 @@ def make_workload(name: str, rank: int, n: int, dev, length: int | None = None):
         out = torch.empty(n, dtype=torch.int32, device=dev)
         step = lambda: rea.crc32_batch(data, stride=L, length=L, count=n, out=out)  # noqa: E731
         return step, n * L, n, out, ("uniform", data, L, L, n)
-    lengths = ragged_lengths(ENET_SEED + rank, n)
+    if name == "frag":
+        # n 64-KiB payloads as the reference sends them (SURVEY.md 8(a) note): each is
+        # fragmented into 49 datagrams at the default MTU, 48 of 1392 B (fragment payload
+        # MTU - 32 = 1360 B plus 32 B of headers, src/c/peer.rs:181-192) and one of
+        # 256 + 32 = 288 B, one checksum per datagram; packed back to back.
+        lengths = np.tile(np.array([1392] * 48 + [288], dtype=np.uint32), n)
+    else:
+        lengths = ragged_lengths(ENET_SEED + rank, n)
     offsets = packed_offsets(lengths)
     total = int(lengths.sum())
     if name == "range":
@@ -138,9 +145,9 @@ def make_workload(name: str, rank: int, n: int, dev, length: int | None = None):
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
     off = torch.from_numpy(offsets.astype(np.int64)).to(dev)
     ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
-    out = torch.empty(n, dtype=torch.int32, device=dev)
+    out = torch.empty(lengths.size, dtype=torch.int32, device=dev)
     step = lambda: rea.crc32_batch(data, offsets=off, lengths=ln, out=out)  # noqa: E731
-    return step, total, n, out, ("ragged", data, offsets, lengths)
+    return step, total, lengths.size, out, ("ragged", data, offsets, lengths)
 
 
 def verify_sample(out, spec, limit=20000) -> None:
@@ -504,7 +511,7 @@ def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, bar
     the N = 1 line carries the other BASELINE configs' per-GPU shapes next to G1."""
     import torch
 
-    step, nbytes, _, out, spec = make_workload(name, rank, n, dev, length=length)
+    step, nbytes, npk, out, spec = make_workload(name, rank, n, dev, length=length)
     step()
     torch.cuda.synchronize()
     verify_sample(out, spec)
@@ -512,7 +519,7 @@ def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, bar
         step()
     wall, kms = time_steps(step, steps, barrier, dev)
     ms = wall * 1000.0 / steps
-    res = {"packets": n, "bytes": nbytes, "ms_per_step": round(ms, 5),
+    res = {"packets": npk, "bytes": nbytes, "ms_per_step": round(ms, 5),
            "value": round(nbytes / (ms / 1000.0) / 2**30, 2), "unit": "GiB/s",
            "kernel_ms": round(kms, 5), "frac": round(nbytes / (kms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
     del spec, out
@@ -598,6 +605,9 @@ def main(argv=None) -> int:
                                           args.warmup, barrier)
         extra["large_64k"] = config_point("large", dev, rank, CONFIGS["large"][1], min(args.steps, 50),
                                           args.warmup, barrier)
+        # The same 32,768 x 64 KiB payloads as the reference checksums them: 49 datagrams each.
+        extra["frag_64k"] = config_point("frag", dev, rank, CONFIGS["large"][1], min(args.steps, 50),
+                                         args.warmup, barrier)
 
     if rank == 0:
         total_bytes = nbytes * world
