@@ -665,9 +665,20 @@ uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, uint32_t new_sl
 // reg(a || b) = M8^n(reg(a) ^ 0xFFFFFFFF) ^ reg(b) with n = |b| (the initial register's
 // share of reg(b) is M8^n(0xFFFFFFFF)), and reg = ~bswap32(checksum), so
 //   checksum(a || b) = bswap32(M8^n(bswap32(crc_a))) ^ crc_b.
-// M8^n by binary powering of M8 as a 32 x 32 GF(2) matrix (column i = M8(1 << i)).
+// M8^n = M8^(n mod 4) M32^(n / 4): byte steps, then the host ladder's M32^(2^k) tables
+// (4 lookups per set bit) while n / 4 < 2^32; beyond that by binary powering of M8 as a
+// 32 x 32 GF(2) matrix (column i = M8(1 << i)).
 uint32_t enet_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
   if (len_b == 0) return crc_a;
+  if ((len_b >> 2) < (1ull << kSlotLevels)) {
+    const uint32_t* l = host_slot_ladder();
+    uint32_t r = __builtin_bswap32(crc_a);
+    for (uint64_t i = 0; i < (len_b & 3u); ++i) r = (r >> 8) ^ kOpTables.sarwate[r & 0xffu];
+    uint64_t q = len_b >> 2;
+    for (int k = 0; q != 0; ++k, q >>= 1)
+      if (q & 1u) r = ladder_apply(l + (size_t)k * kSlotLevelDwords, r);
+    return __builtin_bswap32(r) ^ crc_b;
+  }
   auto apply = [](const uint32_t* m, uint32_t x) {
     uint32_t r = 0;
     for (int i = 0; x != 0; ++i, x >>= 1)

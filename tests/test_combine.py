@@ -53,3 +53,16 @@ def test_combine_shards_and_long_lengths():
         right = rea.crc32_combine(A, rea.crc32_combine(B, C, nc), nb + nc)
         assert left == right
     assert rea.crc32_combine(0x12345678, 0, 0) == 0x12345678
+
+
+def test_combine_ladder_and_matrix_paths_agree():
+    # Lengths below 2^34 take the host ladder (M32^(2^k) tables), longer ones the GF(2)
+    # matrix powering: f(x, n) = combine(x, 0, n) must compose across the switch-over.
+    rng = np.random.default_rng(11)
+    for _ in range(100):
+        x = int(rng.integers(0, 1 << 32, dtype=np.uint64))
+        n1 = (1 << 34) - int(rng.integers(1, 4096))
+        n2 = int(rng.integers(1, 8192))
+        lhs = rea.crc32_combine(rea.crc32_combine(x, 0, n1), 0, n2)
+        assert lhs == rea.crc32_combine(x, 0, n1 + n2), (n1, n2)
+        assert rea.crc32_combine(rea.crc32_combine(x, 0, n2), 0, n1) == lhs
