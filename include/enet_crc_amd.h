@@ -214,7 +214,7 @@ ENET_CRC_API uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, ui
                                              uint32_t bytes_after_slot);
 
 /*
- * Host-side merge (no device work; O(log len_b) GF(2) operator squarings).  Given the
+ * Host-side merge (no device work; O(log len_b) table steps; GF(2) matrix squarings past 16 GiB).  Given the
  * checksums crc_a = crc32(&[a]) and crc_b = crc32(&[b]) in the reference's convention
  * (src/crc32.rs:46, bswap32(~reg)), returns crc32(&[a, b]), the checksum of the
  * concatenation, where len_b is the byte length of b (any u64).  This is the merged
