@@ -49,6 +49,14 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t* __restrict__ buf, u
     // 64-KiB kernel's shape), 8 = the same 10 KiB read as contiguous KiB.
     if (PAT == 6) return base + (rr * 8 + g) * 1280 + (uint64_t)s * 128 + 16 * k;
     if (PAT == 8) return base + rr * 10240 + (uint64_t)s * 1024 + lane * 16;
+    // 1200-B packets with every line of the round's 75 read once, whole: group g takes
+    // lines [1200 g / 128, 1200 (g + 1) / 128) of the 9600-B round (9 or 10 lines; a 10th
+    // slot of a 9-line group re-reads the buffer's first line, L2-resident): the shape a
+    // line-split DMA ring with the shared boundary line handed between groups would have.
+    if (PAT == 9) {
+      const uint32_t l0 = (1200u * g) / 128u, l1 = (1200u * (g + 1)) / 128u, line = l0 + (uint32_t)s;
+      return line >= l1 ? base + 16 * k : base + rr * 9600 + (uint64_t)line * 128 + 16 * k;
+    }
     if (PAT == 5) {  // 16 lanes per packet: slots 0-4 packets 0-3 of the round, slots 5-9 packets 4-7
       const uint64_t pk = rr * 8 + (s / 5) * 4 + lane / 16;
       int64_t off = -80 + 256 * (s % 5) + 16 * (int)(lane % 16);
@@ -334,6 +342,17 @@ int main() {
       run_fn(probe_linesplit<2>, "line-split, nt except shared lines", d, npk, out, cus);
       run_fn(probe_linesplit<0>, "line-split, plain", d, npk, out, cus);
       run_fn(probe_linesplit<1>, "line-split, all nt", d, npk, out, cus);
+    }
+    return 0;
+  }
+  if (getenv("PROBE_SHARED")) {  // G1 bytes: each line once (P9) vs the kernel's shape, vs P6
+    const uint64_t n6 = npk * 1200 / 1280;
+    for (int rep = 0; rep < 2; ++rep) {
+      run<1, 2, 0, 5>("P1 kernel shape, kernel lookups (DMA)", d, npk, out, cus);
+      run_fn(probe_linesplit<0>, "line-split register ring, plain", d, npk, out, cus);
+      run<9, 2, 0, 5>("P9 G1 lines once, kernel lookups", d, npk, out, cus);
+      run<9, 2, 1, 5>("P9 G1 lines once, kernel lookups nt", d, npk, out, cus);
+      run<6, 2, 1, 5>("P6 1280-B lines, kernel lookups nt", d, n6, out, cus);
     }
     return 0;
   }
