@@ -165,18 +165,13 @@ struct Batch {
   uint64_t stride;
   uint32_t length;
   uint64_t count;
-  const uint32_t* perm = nullptr;  // ragged: optional processing order (packet ids sorted by step count)
 };
 
-// Packet id processed in position p (the identity unless the batch is permuted).
+// Packet id processed in position p (past the end: the last packet, read as empty).
 template <bool kRagged>
 __device__ __forceinline__ uint64_t packet_id(const Batch<kRagged>& b, uint64_t p) {
-  if constexpr (kRagged) {
-    const uint64_t q = p < b.count ? p : b.count - 1;
-    return b.perm ? (uint64_t)b.perm[q] : q;
-  } else {
-    return p;
-  }
+  if constexpr (kRagged) return p < b.count ? p : b.count - 1;
+  return p;
 }
 
 // Descriptor of the packet in position p (p >= count reads as an empty packet).
@@ -437,7 +432,7 @@ __global__ __launch_bounds__(kBlock) void crc32_rounds_kernel(Batch<kRagged> b, 
 // Streaming kernel: any packet lengths.  Each round (8 packets of a wave) is padded
 // to T = ceil(max nsteps / U) * U slots and streamed through a U-deep ring.
 // ---------------------------------------------------------------------------------
-// The rounds of one wave (`lds` filled by fill_lds); also the flat path's fallback.
+// The rounds of one wave (`lds` filled by fill_lds).
 template <int U, bool kRagged>
 __device__ __forceinline__ void stream_rounds(const uint32_t* lds, const Batch<kRagged>& b, uint32_t* __restrict__ out) {
   const LaneConsts c = lane_consts(b.base);
@@ -508,116 +503,8 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
   stream_rounds<U, kRagged>(lds, b, out);
 }
 
-// ---------------------------------------------------------------------------------
-// Ragged batches: order the packets by step count first (a counting sort on device),
-// so the 8 packets of a streaming-kernel round need the same number of slots instead
-// of all being padded to the longest.  Two small kernels, O(12 B) per packet:
-//   hist:    per-workgroup histogram of step classes over a contiguous packet range,
-//            stored class-major (hist[class * G + block]);
-//   records (or scatter): same ranges; each block first derives its output position
-//            per class from the whole histogram (block_class_bases: the exclusive scan
-//            in class-major order), then writes round records (perm[position] = id).
-// ---------------------------------------------------------------------------------
-constexpr int kStepClasses = 16;  // class = min(nsteps, 15)
-constexpr int kSortBlock = 256;
+constexpr int kStepClasses = 16;  // ragged sort key: class = min(nsteps, 15)
 
-__device__ __forceinline__ uint32_t step_class_of(uint64_t sa, uint32_t len) {
-  const int32_t ns = make_geo(sa, len).nsteps;
-  return (uint32_t)(ns < kStepClasses - 1 ? ns : kStepClasses - 1);
-}
-
-__device__ __forceinline__ uint32_t step_class(const Batch<true>& b, uint64_t p) {
-  return step_class_of(b.base + b.offsets[p], b.lengths[p]);
-}
-
-// The sort kernels give every thread up to kSortPer packets of its block's range;
-// all their descriptors are loaded before any is used (one memory latency, not kSortPer).
-constexpr int kSortPer = 8;
-
-__device__ __forceinline__ void sort_range(uint64_t count, uint64_t& lo, uint64_t& hi) {
-  const uint64_t per = (count + gridDim.x - 1) / gridDim.x;
-  lo = (uint64_t)blockIdx.x * per;
-  hi = lo + per < count ? lo + per : count;
-}
-
-__global__ __launch_bounds__(kSortBlock) void crc32_class_hist_kernel(Batch<true> b, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[kStepClasses];
-  if (threadIdx.x < kStepClasses) h[threadIdx.x] = 0;
-  __syncthreads();
-  uint64_t lo, hi;
-  sort_range(b.count, lo, hi);
-  for (uint64_t p0 = lo + threadIdx.x; p0 < hi; p0 += kSortBlock * kSortPer) {
-    uint64_t off[kSortPer];
-    uint32_t len[kSortPer];
-#pragma unroll
-    for (int k = 0; k < kSortPer; ++k) {
-      const uint64_t p = p0 + (uint64_t)k * kSortBlock;
-      off[k] = p < hi ? b.offsets[p] : 0;
-      len[k] = p < hi ? b.lengths[p] : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kSortPer; ++k)
-      if (p0 + (uint64_t)k * kSortBlock < hi) atomicAdd(&h[step_class_of(b.base + off[k], len[k])], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < kStepClasses) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
-}
-
-// First output position of this block's packets of each class, straight from the
-// class-major histogram (no separate scan launch): position(c, b) = sum of all counts of
-// classes < c + counts of class c in blocks < b.  Thread t reads hist[c][t + 256 k]
-// for every class (16 x G/256 loads); the 32 sums (totals, and partials over blocks
-// < blockIdx) are reduced per wave with shuffles and across the 4 waves in LDS.
-__device__ __forceinline__ void block_class_bases(const uint32_t* __restrict__ hist, uint32_t* cur) {
-  __shared__ uint32_t red[kSortBlock / 64][2 * kStepClasses];
-  const uint32_t G = gridDim.x, t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  uint32_t tot[kStepClasses], part[kStepClasses];
-#pragma unroll
-  for (int c = 0; c < kStepClasses; ++c) tot[c] = part[c] = 0;
-  for (uint32_t bb = t; bb < G; bb += kSortBlock) {
-    uint32_t h[kStepClasses];
-#pragma unroll
-    for (int c = 0; c < kStepClasses; ++c) h[c] = hist[c * G + bb];
-#pragma unroll
-    for (int c = 0; c < kStepClasses; ++c) {
-      tot[c] += h[c];
-      part[c] += bb < blockIdx.x ? h[c] : 0u;
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < kStepClasses; ++c) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      tot[c] += (uint32_t)__shfl_xor((int)tot[c], d, 64);
-      part[c] += (uint32_t)__shfl_xor((int)part[c], d, 64);
-    }
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < kStepClasses; ++c) {
-      red[w][c] = tot[c];
-      red[w][kStepClasses + c] = part[c];
-    }
-  }
-  __syncthreads();
-  if (t < kStepClasses) {
-    uint32_t base = 0;
-    for (uint32_t c = 0; c < t; ++c)
-      for (uint32_t q = 0; q < kSortBlock / 64; ++q) base += red[q][c];
-    for (uint32_t q = 0; q < kSortBlock / 64; ++q) base += red[q][kStepClasses + t];
-    cur[t] = base;
-  }
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(kSortBlock) void crc32_class_scatter_kernel(Batch<true> b, const uint32_t* __restrict__ hist,
-                                                                          uint32_t* __restrict__ perm) {
-  __shared__ uint32_t cur[kStepClasses];
-  block_class_bases(hist, cur);
-  uint64_t lo, hi;
-  sort_range(b.count, lo, hi);
-  for (uint64_t p = lo + threadIdx.x; p < hi; p += kSortBlock) perm[atomicAdd(&cur[step_class(b, p)], 1u)] = (uint32_t)p;
-}
 
 // Round records for crc32_ragged_dma_kernel: sorted position q = 8 r + g goes to
 // record r, group g.  128 B per round, per group: the packet's geometry precomputed
@@ -784,7 +671,6 @@ struct UniformBatch {
   uint64_t stride;
   uint32_t length;
   uint64_t count;
-  uint32_t xcd_swizzle = 0;  // ENET_CRC_XCD=1: XCD-aware round order (A/B runs; off: DESIGN.md §6)
 };
 
 // ---------------------------------------------------------------------------------
@@ -888,17 +774,6 @@ __device__ __forceinline__ void horner_step_and_read(const Lookup& lk, uint32_t&
       : "memory");
 }
 
-// Logical block index under which the workgroups sharing an XCD (blockIdx % 8, as the
-// dispatcher is observed to place them) get consecutive indices, i.e. neighbouring
-// packets: the 128-B line two packets of adjacent rounds share is then fetched into one
-// XCD's L2 instead of two (bijective for any grid: cdna_hip_programming.md §5.5 T1).
-__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t orig, uint32_t nwg) {
-  constexpr uint32_t kXcds = 8;
-  if (nwg <= kXcds) return orig;
-  const uint32_t q = nwg / kXcds, r = nwg % kXcds, xcd = orig % kXcds;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / kXcds;
-}
-
 // LDS atomic add in asm: hipcc would otherwise order it behind every in-flight LDS-DMA
 // (it cannot tell the counter from the ring) and drain the ring with vmcnt(0).
 __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
@@ -920,9 +795,8 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 // a CU finished up to 1.5x later than the oldest, leaving the CU
 // half-occupied at the end.  A wave knows its next kLook rounds ahead of time (the
 // ring prefetches that far) and fetches one more per round.
-// NS > 0: packets of exactly NS steps, the slot loop fully unrolled.  NS == 0: any
-// step count >= kDmaRing (long packets, e.g. 64 KiB buffers: 512 steps), slot loop
-// unrolled by the ring depth.
+// Packets of 15 steps and more (1793 B .. 4 KiB; shorter ones take the register ring,
+// longer ones the wave-per-packet kernel); runtime step count.
 //
 // Trailing bytes: every packet is run to the next 4-byte boundary (Lx = length
 // rounded up), the z = Lx - length bytes past its end are masked to zero in the last
@@ -935,14 +809,14 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 // memory system does fastest (tools/dma_probe PROBE_LINES: 8 aligned lines per
 // instruction with the kernel's lookups, 197 us non-temporal vs 219.5 us plain for
 // 1.26 GB; on lines a packet shares with its neighbour the hint costs a second fetch).
-template <int NS, bool kNT = false>
+template <bool kNT>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   constexpr int kDmaRing = kUniformRing;
   __shared__ __attribute__((aligned(16))) UniformDmaLds<kDmaRing> S;
   uint32_t* const lds = S.tables;
   auto& ring = S.ring;
   uint32_t& next_dispatch = S.next_dispatch;
-  constexpr int kLook = NS > 0 ? 1 + (NS - 1 + kDmaRing) / NS : 2;  // rounds a wave must know ahead
+  constexpr int kLook = 2;  // rounds a wave must know ahead
   if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
   fill_lds(lds);
   __syncthreads();
@@ -952,14 +826,13 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
 
   const uint64_t total_rounds = (u.count + kPacketsPerWave - 1) / kPacketsPerWave;
   const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint32_t lb = u.xcd_swizzle ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
   auto round_of = [&](uint32_t d) -> uint64_t {
-    return (uint64_t)lb * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
   };
 
   const uint32_t lx = (u.length + 3u) & ~3u, z = lx - u.length;
   const PacketGeo g = make_geo(0, lx);
-  const int32_t ns = NS > 0 ? NS : g.nsteps;
+  const int32_t ns = g.nsteps;  // >= kDmaRing (launch_uniform)
   const uint32_t last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;  // lane 0 holds the last word
   // This lane's slot-0 chunk relative to its packet's start (> -128: DESIGN.md §3).
   const int64_t rel0 = (int64_t)g.a1 - 16 * (int64_t)(c.k + 1u) - (int64_t)kBytesPerStep * (ns - 1);
@@ -996,12 +869,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
   if (rnd[0] >= total_rounds) return;
   if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
 #pragma unroll
-  for (int f = 0; f < kDmaRing; ++f) {
-    if constexpr (NS > 0)
-      dma(slot_src(packet_base(rnd[f / NS]), f % NS), (uint32_t)f);
-    else
-      dma(slot_src(packet_base(rnd[0]), f), (uint32_t)f);  // ns >= kDmaRing
-  }
+  for (int f = 0; f < kDmaRing; ++f) dma(slot_src(packet_base(rnd[0]), f), (uint32_t)f);  // ns >= kDmaRing
   uint32_t q = 0;  // ring position of the slot being consumed (wave-uniform)
   // The ring is read one slot ahead: `nextv` holds the slot about to be consumed.
   u32x4 nextv = read_landed_slot<kDmaRing - 1>(ring0 + lane * 16u);
@@ -1012,17 +880,13 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
     uint32_t d = 0;
     if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
     const uint64_t pb = packet_base(rnd[0]);
-    uint64_t pb_next = 0;
-    if constexpr (NS == 0) pb_next = packet_base(rnd[1]);
+    const uint64_t pb_next = packet_base(rnd[1]);
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     // One slot: wait for it, refill its LDS slot kDmaRing slots ahead, then the lookups.
     auto slot = [&](int32_t s, bool top, bool last) {
       const u32x4 v = nextv;
       const int32_t f = s + kDmaRing;  // refill this slot's LDS slot kDmaRing slots ahead
-      if constexpr (NS > 0)
-        dma(slot_src(packet_base(rnd[f / NS]), f % NS), q);  // f / NS, f % NS fold to constants
-      else
-        dma(f < ns ? slot_src(pb, f) : slot_src(pb_next, f - ns), q);
+      dma(f < ns ? slot_src(pb, f) : slot_src(pb_next, f - ns), q);
       q = q + 1 == (uint32_t)kDmaRing ? 0u : q + 1;
       const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
       uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
@@ -1044,14 +908,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
       }
       issue_order_fence();  // keep each slot's lookups between its DMA and the next slot's wait
     };
-    if constexpr (NS > 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) slot(s, s == 0, s == NS - 1);
-    } else {
-      slot(0, true, false);  // ns >= kDmaRing > 1
-      for (int32_t s = 1; s < ns - 1; ++s) slot(s, false, false);
-      slot(ns - 1, false, true);
-    }
+    slot(0, true, false);  // ns >= kDmaRing > 1
+    for (int32_t s = 1; s < ns - 1; ++s) slot(s, false, false);
+    slot(ns - 1, false, true);
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, z, c.lk);  // every lane; lane k == 0 holds the register
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
@@ -1242,20 +1101,15 @@ __global__ __launch_bounds__(kBlock) void crc32_wave_dma_kernel(UniformBatch u, 
 }
 
 // ---------------------------------------------------------------------------------
-// Uniform kernel, register form (ENET_CRC_UNIFORM=regs).  Same geometry, arithmetic,
-// dispatch, result batching and trailing-byte handling as crc32_uniform_dma_kernel,
-// but the packet bytes go straight to VGPRs: the next round's NS chunks are loaded
-// into the ring registers while this round's are consumed (NS KiB per wave in flight)
-// and LDS serves only the table lookups (no DMA write, no ring read).  Every load is
-// unconditional and issued in slot order, so hipcc's waitcnts stay exact.
-// ---------------------------------------------------------------------------------
-struct UniformRegsLds {
-  uint32_t tables[kLdsDwords];
-  uint32_t next_dispatch;
-};
-
+// Uniform kernel, register form: the G1 path (packets of 1..14 steps, <= 1792 B).  Same
+// geometry, arithmetic, dispatch, result batching and trailing-byte handling as
+// crc32_uniform_dma_kernel, but the packet bytes go straight to VGPRs: the next round's
+// chunks are loaded into the ring registers while this round's are consumed (NS + 1
+// KiB per wave in flight) and LDS serves only the table lookups (no DMA write, no ring
+// read).  Every load is unconditional and issued in slot order, so hipcc's waitcnts
+// stay exact.
 //
-// kSplit (line-split loads): the ring has NS + 1 entries and each load reads, per group,
+// Line-split loads: the ring has NS + 1 entries and each load reads, per group,
 // the chunks of ONE 128-B line (aligned to the packet end's 16-B residue) instead of one
 // end-aligned 128-B piece, which straddles two lines.  A piece i of the packet (end at
 // a1, j = (a1 mod 128) / 16) is the top 8 - j chunks of one line plus the bottom j of the
@@ -1264,7 +1118,13 @@ struct UniformRegsLds {
 // lookups; one more load per round, but 8 whole lines per load instruction instead of
 // 16 partial ones (tools/dma_probe PROBE_SPLIT: 217-219 us vs 224-229 us for the piece
 // loads, same box, alternating).
-template <int NS, bool kSplit = false>
+// ---------------------------------------------------------------------------------
+struct UniformRegsLds {
+  uint32_t tables[kLdsDwords];
+  uint32_t next_dispatch;
+};
+
+template <int NS>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
@@ -1305,16 +1165,12 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 
   uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
   if (rnd0 >= total_rounds) return;
-  constexpr int NE = kSplit ? NS + 1 : NS;  // ring entries
+  constexpr int NE = NS + 1;  // ring entries
   // Ring entry e of the round whose packet (this group's) starts at pb.
   auto entry_src = [&](uint64_t pb, int e) -> uint64_t {
-    if constexpr (!kSplit) {
-      return slot_src(pb, e);
-    } else {
-      const uint32_t lo = c.k < ((uint32_t)(pb + lx) & 127u) >> 4 ? 1u : 0u;
-      const int32_t sl = e - (int32_t)lo;
-      return sl < 0 || sl >= NS ? c.dummy : slot_src(pb, sl);
-    }
+    const uint32_t lo = c.k < ((uint32_t)(pb + lx) & 127u) >> 4 ? 1u : 0u;
+    const int32_t sl = e - (int32_t)lo;
+    return sl < 0 || sl >= NS ? c.dummy : slot_src(pb, sl);
   };
   u32x4 q[NE];
   {
@@ -1331,12 +1187,11 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
     uint32_t d = 0;
     if (lane == 0) d = atomicAdd(&S.next_dispatch, 1u);
     const uint64_t pb = packet_base(rnd0), pbn = packet_base(rnd1);
-    const bool lo = kSplit && c.k < (((uint32_t)(pb + lx) & 127u) >> 4);
+    const bool lo = c.k < (((uint32_t)(pb + lx) & 127u) >> 4);
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      u32x4 v = q[s];
-      if constexpr (kSplit) v = lo ? q[s + 1] : q[s];
+      const u32x4 v = lo ? q[s + 1] : q[s];
       uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
       if (s == 0) {
         const bool below = is_below(pb);
@@ -1360,10 +1215,8 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
       q[s] = load_chunk(entry_src(pbn, s));  // the next round's entry s
       issue_order_fence();
     }
-    if constexpr (kSplit) {
-      q[NS] = load_chunk(entry_src(pbn, NS));
-      issue_order_fence();
-    }
+    q[NS] = load_chunk(entry_src(pbn, NS));
+    issue_order_fence();
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, z, c.lk);  // every lane; lane k == 0 holds the register
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
@@ -1401,7 +1254,6 @@ struct RaggedDmaBatch {
   const uint8_t* recs;  // round records
   uint64_t count;
   uint32_t xcd_rounds;  // grid multiple of 8: sweep s of XCD x = one contiguous record range
-  uint32_t top0_only;   // ENET_CRC_FASTTOP=0: short-packet rounds take the generic path (A/B)
 };
 
 struct RaggedRound {
@@ -1605,7 +1457,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
     // round reads as zeros (ragged_src with !direct).
     rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
     rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform || (rr.meta & kMetaFallback)) &&
-              rr.ns <= kRaggedFastMax && !(b.top0_only && rr.top_uniform != 0);
+              rr.ns <= kRaggedFastMax;
     return rr;
   };
 
@@ -1666,729 +1518,6 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
   __builtin_amdgcn_s_waitcnt(0);
 }
 
-// ---------------------------------------------------------------------------------
-// Group-stream kernel: ragged batches in their own order, no pre-pass.
-//
-// The 8 groups of a wave are independent consumers of one in-order packet queue:
-// when a group finishes a packet it takes the next unassigned one (ballot rank, no
-// atomics), so a group never waits for the others and no slot is padded to a round's
-// longest packet.  Consecutive packets are in flight in neighbouring groups at the
-// same time, so the 128-B line two packets share is read twice within a few steps
-// (from L2), not twice from HBM as after a sort by length.
-//
-// Pipeline per wave (kGsRing slots of 1 KiB in a register ring; the slot loop is
-// unrolled by the ring depth so every ring register is statically indexed):
-//   producer, kGsRing steps ahead: assign packets to groups without one, issue each
-//     lane's 16-B load (global_load_dwordx4, unconditional: chunks outside a packet
-//     read the zero chunk) and the step's metadata (top-word masking, last step, id);
-//   consumer: mask, one Horner step on the 4 word streams (same arithmetic and tables
-//     as every other kernel here), and at a packet's last step PARK the group's 4x8
-//     stream values in LDS at the next column of a wave-wide park row, then zero them.
-//     When a row holds 8 packets, one combine pass turns it into 8 checksums with every
-//     lane busy (combine_streams: in-lane Horner + DPP tree inside 8-lane groups).
-// Work distribution: tasks of kGsTask consecutive packets; workgroup b owns tasks
-// b*16 + j + i*16*grid and its waves claim them in order from an LDS counter; the
-// groups of a wave flow from one claimed task into the next without synchronising.
-// Descriptors: once per ring cycle every lane reloads two (offset, length) pairs of the
-// next kGsAhead tasks into the wave's LDS ring of task buffers (rewrites of unchanged
-// entries are harmless).  The queue advances at most 8 packets per step, i.e. at most
-// 3 tasks per cycle, so the tasks it reaches in a cycle were written by the previous
-// cycle's reload: no wait, and every load stays unconditional (hipcc's vmcnt exact).
-// ---------------------------------------------------------------------------------
-constexpr int kGsRing = 5;                               // slots in flight per wave
-constexpr int kGsTask = 16;                              // packets per task
-constexpr int kGsAhead = 2 * 64 / kGsTask;               // tasks one reload covers (2 per lane)
-constexpr int kGsBufs = kGsAhead + 1;                    // task buffers (the current one + kGsAhead)
-static_assert((kGsTask - 1 + 8 * kGsRing) / kGsTask + 3 <= kGsAhead, "a cycle reaches only reloaded tasks");
-constexpr uint32_t kGsHead = 1u << 0;                    // lane's chunk holds the packet's top word
-constexpr uint32_t kGsJ0Shift = 1;                       // 2 bits: index of the top word in the chunk
-constexpr uint32_t kGsVShift = 3;                        // 2 bits: sa - top
-constexpr uint32_t kGsLast = 1u << 5;                    // last step of the group's packet
-constexpr uint32_t kGsZShift = 6;                        // 2 bits: bytes run past the packet end (lane 0)
-constexpr uint32_t kGsFallback = 1u << 8;                // chunk begins before the caller's buffer
-constexpr uint32_t kGsFbShift = 9;                       // 2 bits: (chunk - (base4 - 16)) / 4
-constexpr uint32_t kGsIdle = 0xFFFFFFFFu;                // group has no packet and will get none
-
-struct GsLds {
-  uint32_t tables[kLdsDwords];
-  uint64_t doff[kWavesPerBlock][kGsBufs][kGsTask];
-  uint32_t dlen[kWavesPerBlock][kGsBufs][kGsTask];
-  u32x4 park[kWavesPerBlock][2][64];
-  uint32_t pmeta[kWavesPerBlock][2][8][2];  // packet id, z
-  uint64_t claim[kWavesPerBlock][kGsBufs];  // task of sequence number s at [s % kGsBufs]
-  uint32_t next_dispatch;
-};
-static_assert(sizeof(GsLds) <= 160 * 1024, "LDS");
-
-struct GsBatch {
-  uint64_t base;
-  const uint64_t* offsets;
-  const uint32_t* lengths;
-  uint64_t count;
-};
-
-typedef __attribute__((address_space(1))) const uint64_t GlobalU64;
-typedef __attribute__((address_space(1))) uint32_t GlobalOutU32;
-
-__global__ __launch_bounds__(kBlock) void crc32_group_stream_kernel(GsBatch batch, uint32_t* out_ptr) {
-  __shared__ __attribute__((aligned(16))) GsLds S;
-  // The batch in locals (lambdas capture these, not the by-value kernel argument) and
-  // global-address-space pointers (global_load/store, never flat: flat ops count on
-  // lgkmcnt too and would order against the LDS lookups).
-  const uint64_t base = batch.base, count = batch.count;
-  GlobalU64* const offsets = (GlobalU64*)batch.offsets;
-  GlobalU32* const lengths = (GlobalU32*)batch.lengths;
-  GlobalOutU32* const out = (GlobalOutU32*)out_ptr;
-  uint32_t* const lds = S.tables;
-  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kGsBufs;
-  fill_lds(lds);
-  __syncthreads();
-  const LaneConsts c = lane_consts(base);
-  const uint32_t lane = threadIdx.x & 63u, k = c.k, lead = lane & ~7u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t ntasks = (count + kGsTask - 1) / kGsTask;
-  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
-  auto task_of = [&](uint32_t d) __attribute__((always_inline)) -> uint64_t {
-    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
-  };
-  // Claimed tasks: S.claim holds the tasks of sequence numbers seq .. seq + kGsAhead;
-  // tk0 / tk1 (wave-uniform) are those of seq and seq + 1.
-  const uint64_t tk_first = task_of(wv);
-  if (tk_first >= ntasks) return;
-  if (lane < (uint32_t)kGsBufs) S.claim[wv][lane] = task_of(wv + kWavesPerBlock * lane);
-  uint64_t tk0 = tk_first, tk1 = task_of(wv + kWavesPerBlock);
-  uint32_t seq = 0;  // sequence number of tk0 (the task the queue is in)
-  uint32_t idx = 0;  // queue position inside tk0
-
-  auto desc_src = [&](uint64_t t, uint32_t i) __attribute__((always_inline)) -> uint64_t {
-    const uint64_t p = t * kGsTask + i;
-    return p < count ? p : count - 1;
-  };
-  // Reload: lane l, pair r -> packet l % kGsTask of the task seq + 1 + l / kGsTask + 4r.
-  uint64_t ld_off0 = 0, ld_off1 = 0;
-  uint32_t ld_len0 = 0, ld_len1 = 0, ld_seq = 0;
-  const uint32_t di = lane % kGsTask, da = lane / kGsTask;
-  auto desc_issue = [&]() __attribute__((always_inline)) {
-    const uint64_t t0 = S.claim[wv][(seq + 1 + da) % kGsBufs];
-    const uint64_t t1 = S.claim[wv][(seq + 5 + da) % kGsBufs];
-    const uint64_t p0 = desc_src(t0, di), p1 = desc_src(t1, di);
-    ld_off0 = offsets[p0];
-    ld_len0 = lengths[p0];
-    ld_off1 = offsets[p1];
-    ld_len1 = lengths[p1];
-    ld_seq = seq;
-  };
-  auto desc_commit = [&]() __attribute__((always_inline)) {
-    const uint32_t s0 = ld_seq + 1 + da, s1 = ld_seq + 5 + da;
-    S.doff[wv][s0 % kGsBufs][di] = ld_off0;
-    S.dlen[wv][s0 % kGsBufs][di] = ld_len0;
-    S.doff[wv][s1 % kGsBufs][di] = ld_off1;
-    S.dlen[wv][s1 % kGsBufs][di] = ld_len1;
-  };
-  {  // the current task's descriptors, then the reload of the next kGsAhead
-    const uint64_t p0 = desc_src(tk0, di);
-    const uint64_t o0 = offsets[p0];
-    const uint32_t l0 = lengths[p0];
-    S.doff[wv][0][di] = o0;
-    S.dlen[wv][0][di] = l0;
-  }
-  desc_issue();
-  desc_commit();
-
-  // ---- producer state (group-uniform values in every lane of the group) ----
-  uint64_t pa = 0;         // this lane's chunk address at the group's next step
-  uint32_t rem = 0;        // steps left in the group's packet (0: needs one)
-  uint32_t pid = 0;        // packet id, or kGsIdle
-  uint32_t topf = 0;       // flags of the packet's first step
-  uint32_t zl = 0;         // z << kGsZShift of the packet (for its last step)
-  bool first = false;      // next step is the packet's first
-  bool top_dummy = false;  // this lane reads the zero chunk at the first step
-
-  // Give every group that needs a packet the next one in queue order (at most 8 per
-  // step).  An empty packet is answered on the spot; its group takes another next step.
-  auto assign = [&]() __attribute__((always_inline)) {
-    const uint64_t need = __builtin_amdgcn_ballot_w64(k == 0 && rem == 0 && pid != kGsIdle);
-    if (need == 0) return;
-    const bool mine = (need >> lead) & 1ull;
-    const uint32_t pos = idx + (uint32_t)__builtin_popcountll(need & ((1ull << lead) - 1ull));
-    if (mine) {
-      const uint32_t tsel = pos / kGsTask;  // 0: tk0, 1: tk1 (pos < 2 kGsTask)
-      const uint64_t t = tsel ? tk1 : tk0;
-      const uint32_t i = pos % kGsTask;
-      const uint64_t p = t * kGsTask + i;
-      if (t >= ntasks || p >= count) {
-        pid = kGsIdle;  // the queue is exhausted: nothing follows in this wave
-      } else {
-        const uint32_t buf = (seq + tsel) % kGsBufs;
-        const uint64_t sa = base + S.doff[wv][buf][i];
-        const uint32_t len = S.dlen[wv][buf][i];
-        pid = (uint32_t)p;
-        if (len == 0) {
-          if (k == 0) out[p] = 0u;  // crc32(&[]) == 0 (src/crc32.rs:40,46)
-        } else {
-          const uint64_t ea = sa + len;
-          const uint32_t z = (4u - (uint32_t)(ea & 3u)) & 3u;
-          const uint64_t ex = ea + z, top = sa & ~(uint64_t)3;
-          const uint64_t nwords = (ex - top) >> 2;
-          const uint32_t ns = (uint32_t)((((nwords + 3) >> 2) + kLanesPerPacket - 1) / kLanesPerPacket);
-          const uint64_t c0 = ex - 16u * (uint64_t)(k + 1u) - (uint64_t)kBytesPerStep * (ns - 1u);
-          const int64_t rel0 = (int64_t)(c0 - top);
-          const bool head = rel0 > -16 && rel0 <= 0;
-          const bool fb = head && c0 < c.base4;
-          uint32_t f = 0;
-          if (head) {
-            f = kGsHead | ((uint32_t)(-rel0 >> 2) << kGsJ0Shift) | ((uint32_t)(sa - top) << kGsVShift);
-            if (fb) f |= kGsFallback | ((uint32_t)((c0 + 16u - c.base4) >> 2) << kGsFbShift);
-          }
-          pa = c0;
-          rem = ns;
-          topf = f;
-          zl = z << kGsZShift;
-          first = true;
-          top_dummy = rel0 <= -16 || fb;
-        }
-      }
-    }
-    idx += (uint32_t)__builtin_popcountll(need);
-    if (idx >= (uint32_t)kGsTask) {  // into the next claimed task
-      idx -= kGsTask;
-      ++seq;
-      uint32_t d = 0;
-      if (lane == 0) {
-        d = atomicAdd(&S.next_dispatch, 1u);
-        S.claim[wv][(seq + kGsAhead) % kGsBufs] = task_of(d);
-      }
-      tk0 = tk1;
-      const uint64_t t1 = S.claim[wv][(seq + 1) % kGsBufs];
-      tk1 = __builtin_amdgcn_readfirstlane((uint32_t)t1) |
-            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t1 >> 32)) << 32);
-    }
-  };
-
-  // One producer step: the load and metadata of the group's next step into a ring slot.
-  auto produce = [&](u32x4& data, uint32_t& flags, uint32_t& id) __attribute__((always_inline)) {
-    assign();
-    const bool active = rem > 0;
-    uint64_t src = active && !(first && top_dummy) ? pa : c.dummy;
-    asm volatile("" : "+v"(src));  // ONE unconditional load (hipcc would otherwise branch between two)
-    uint32_t f = first ? topf : 0u;
-    if (active && rem == 1) f |= kGsLast | zl;
-    data = load_chunk(src);
-    flags = f;
-    id = pid;
-    pa += active ? (uint64_t)kBytesPerStep : 0u;  // branch-free: keeps the load out of any branch
-    rem -= active ? 1u : 0u;
-    first = false;
-    issue_order_fence();
-  };
-
-  // ---- consumer state ----
-  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-  uint32_t parked = 0;  // packets parked so far by this wave (row = (parked / 8) % 2)
-
-  auto combine_row = [&](uint32_t row, uint32_t ncols) __attribute__((always_inline)) {
-    const u32x4 hv = S.park[wv][row][lane];
-    const uint32_t col = lane >> 3;
-    const uint32_t id = S.pmeta[wv][row][col][0], z = S.pmeta[wv][row][col][1];
-    const uint32_t y = combine_tree(lds, hv.x, hv.y, hv.z, hv.w, c.lk);
-    uint32_t reg = finish_word(lds, y, z, c.lk);  // lane k == 0 holds the register
-    if (k == 0 && col < ncols) out[id] = __builtin_bswap32(~reg);
-  };
-
-  auto consume = [&](const u32x4& data, uint32_t f, uint32_t id) __attribute__((always_inline)) {
-    uint32_t w0 = data.x, w1 = data.y, w2 = data.z, w3 = data.w;
-    const uint32_t j0 = (f >> kGsJ0Shift) & 3u;
-    if (__builtin_amdgcn_ballot_w64(f & kGsFallback)) {
-      if (f & kGsFallback) {
-        const uint64_t chunk = c.base4 - 16u + 4u * ((f >> kGsFbShift) & 3u);
-        load_top_words(chunk, 4u - j0, c.dummy, w0, w1, w2, w3);
-      }
-    }
-    const bool last = (f & kGsLast) != 0;
-    if (last && k == 0) w3 &= 0xFFFFFFFFu >> (8u * ((f >> kGsZShift) & 3u));  // data only, before injection
-    if (__builtin_amdgcn_ballot_w64(f & kGsHead)) {
-      if (f & kGsHead) mask_top((4u - j0) | (((f >> kGsVShift) & 3u) << kMetaVShift), w0, w1, w2, w3);
-    }
-    h0 = horner_main(lds, h0, w0, c.lk);
-    h1 = horner_main(lds, h1, w1, c.lk);
-    h2 = horner_main(lds, h2, w2, c.lk);
-    h3 = horner_main(lds, h3, w3, c.lk);
-    const uint64_t ends = __builtin_amdgcn_ballot_w64(last && k == 0);
-    if (ends) {
-      if (last) {
-        const uint32_t pos = parked + (uint32_t)__builtin_popcountll(ends & ((1ull << lead) - 1ull));
-        const uint32_t row = (pos >> 3) & 1u, col = pos & 7u;
-        S.park[wv][row][col * 8u + k] = u32x4{h0, h1, h2, h3};
-        if (k == 0) {
-          S.pmeta[wv][row][col][0] = id;
-          S.pmeta[wv][row][col][1] = (f >> kGsZShift) & 3u;
-        }
-        h0 = h1 = h2 = h3 = 0;
-      }
-      const uint32_t before = parked;
-      parked += (uint32_t)__builtin_popcountll(ends);
-      if ((before ^ parked) & ~7u) combine_row((before >> 3) & 1u, 8u);  // a row is full
-    }
-  };
-
-  // ---- main loop ----
-  u32x4 ring[kGsRing];
-  uint32_t rflags[kGsRing], rid[kGsRing];
-#pragma unroll
-  for (int q = 0; q < kGsRing; ++q) produce(ring[q], rflags[q], rid[q]);
-  uint32_t idle_slots = 0;  // consecutive producer steps with every group idle
-  for (;;) {
-    desc_issue();  // this ring cycle's descriptor reload (written at its end)
-#pragma unroll
-    for (int q = 0; q < kGsRing; ++q) {
-      const u32x4 data = ring[q];
-      const uint32_t f = rflags[q], id = rid[q];
-      consume(data, f, id);
-      produce(ring[q], rflags[q], rid[q]);
-      idle_slots = __builtin_amdgcn_ballot_w64(pid != kGsIdle) ? 0u : idle_slots + 1u;
-    }
-    desc_commit();
-    if (idle_slots >= (uint32_t)kGsRing) break;  // every issued step has been consumed
-  }
-  if (parked & 7u) combine_row((parked >> 3) & 1u, parked & 7u);
-}
-
-// ---------------------------------------------------------------------------------
-// Flat-stream ragged kernels (SURVEY.md §7 "Ragged batch": the batch as one byte
-// stream, cut at fixed positions, packets recovered by linearity).  Default for ragged
-// batches whose packets lie in address order without overlap (gaps <= kFlatMaxGap: a
-// packed receive buffer, or fixed receive slots), which crc32_flat_prep_kernel checks
-// on the device; other batches take the streaming kernel inside the finish launch.
-//
-// Geometry (flat_geo).  The stream [lo, hi) is the packets' span rounded out to 128 B,
-// cut into ngroups regions of spg steps of 128 B.  Region r belongs to group r % 8 of
-// wave r / 8, so every group runs exactly spg steps (no load imbalance, no sort) and a
-// wave's LDS-DMA reads 8 x 128 B from 8 neighbouring regions, the uniform kernel's
-// access shape.  Regions tile the stream: no line is read twice.  Lane k of a group
-// holds bytes [112 - 16k, 128 - 16k) of every step (lane 0 the last 16 B: the order
-// combine_streams assumes).
-//
-// Linear prefix.  Each group runs the uniform kernel's step (4 x 8 word streams,
-// h = M32^32(h) ^ w) over its whole region and never resets: its streams hold
-// G_r(x), the zero-initialised CRC register of the region's bytes [R0, x).  At every
-// packet boundary x (each packet's end; its start too after a gap) it combines the
-// streams with the bytes at and after x removed: E(x) = M8^(T - x) G_r(x), T = the end
-// of the step holding x.  At the region's end, tails[r] = G_r(R1).  Since
-// reg(bytes [s, e)) = G(e) ^ M8^(e - s) G(s) ^ M8^(e - s)(init), the finish pass
-// (one thread per packet) gets every checksum from E(e), E(s), the tails of the
-// regions the packet spans (moved by M8^(multiple of 128) through the forward ladder),
-// one inverse shift M8^-(T - e) (< 128 bytes) and a table of M8^len(init).
-// Descriptors reach a group by LDS-DMA in windows of 8 packets (double-buffered),
-// E(end) values leave 8 at a time (one 32-B store per group).
-// ---------------------------------------------------------------------------------
-constexpr int kFlatRing = 4;                       // LDS slots per wave
-constexpr int kFlatPrepBlock = 256;
-constexpr int kFlatMaxFlags = 1024;                // prep blocks
-constexpr uint32_t kFlatMaxLen = 1u << 28;         // eligibility: packet length
-constexpr uint64_t kFlatMaxGap = 4096;             // eligibility: bytes between neighbours
-constexpr uint64_t kFlatMaxSpg = 1u << 20;         // eligibility: region <= 128 MiB
-constexpr uint32_t kFlatMaxRegionsPerPacket = 64;  // eligibility: bounds a prep thread's work
-constexpr int32_t kFlatFar = 1 << 30;              // position of "no boundary" (past every region)
-constexpr int kFinFwdBase = 5;                     // M32^(32 * 2^i): level 5 + i of the ladder
-constexpr int kFinFwdLds = 8;                      // of which the first 8 are staged in LDS
-
-struct FlatBatch {
-  uint64_t base;
-  const uint64_t* offsets;
-  const uint32_t* lengths;
-  uint64_t count;
-  uint32_t ngroups;        // regions: gridDim.x * 128 of the main kernel
-  uint32_t nflags;         // prep blocks
-  uint32_t* flags;         // [nflags] nonzero: batch not flat-eligible
-  uint32_t* first;         // [ngroups] first packet whose end lies after the region's start
-  uint32_t* tails;         // [ngroups] G_r(R1) of each region
-  uint32_t* e_end;         // [count] E(end of packet)
-  uint32_t* e_start;       // [count] E(start of packet), written only after a gap
-  const uint32_t* ladder;  // device ladder: forward levels, inverse levels, M8^len(init) table
-};
-
-struct FlatGeo {
-  uint64_t lo;      // absolute address of step 0 of region 0
-  uint64_t nsteps;  // steps of the span
-  uint64_t rb;      // bytes per region
-  uint64_t spg;     // steps per region (unclamped: the prep kernel rejects > kFlatMaxSpg)
-};
-
-__device__ __forceinline__ FlatGeo flat_geo(const FlatBatch& b) {
-  const uint64_t s = b.base + b.offsets[0];
-  const uint64_t e = b.base + b.offsets[b.count - 1] + b.lengths[b.count - 1];
-  FlatGeo g;
-  g.lo = s & ~(uint64_t)127;
-  const uint64_t hi = e > g.lo ? (e + 127) & ~(uint64_t)127 : g.lo + 128;
-  g.nsteps = (hi - g.lo) >> 7;
-  g.spg = (g.nsteps + b.ngroups - 1) / b.ngroups;
-  g.rb = (g.spg < kFlatMaxSpg ? g.spg : kFlatMaxSpg) * 128;
-  return g;
-}
-
-// Block-wide: did the prep kernel accept the batch?
-__device__ __forceinline__ bool flat_batch_ok(const FlatBatch& b) {
-  uint32_t bad = 0;
-  for (uint32_t i = threadIdx.x; i < b.nflags; i += blockDim.x) bad |= b.flags[i];
-  return __syncthreads_or(bad) == 0;
-}
-
-// Eligibility (address order, no overlap, gaps <= kFlatMaxGap, lengths < kFlatMaxLen,
-// <= kFlatMaxRegionsPerPacket regions starting inside one packet) and the region map
-// first[r] = min p with end(p) > start(r): packet p (one thread, coalesced loads) writes
-// the regions whose start lies in [end(p-1), end(p)), so in an eligible batch every
-// entry has exactly one writer.  flags[block] = 1 if any packet of the block fails.
-__global__ __launch_bounds__(kFlatPrepBlock) void crc32_flat_prep_kernel(FlatBatch b) {
-  const FlatGeo g = flat_geo(b);
-  const bool small = g.nsteps * 128u + g.rb < (1ull << 32);  // 32-bit divisions suffice
-  const uint32_t rb32 = (uint32_t)g.rb;
-  auto region_ceil = [&](uint64_t rel) -> uint64_t {  // first region starting at or after base + rel
-    const uint64_t x = b.base + rel;
-    if (x <= g.lo) return 0;
-    const uint64_t d = x - g.lo;
-    const uint64_t r = small ? (uint64_t)(((uint32_t)d + rb32 - 1u) / rb32) : (d + g.rb - 1) / g.rb;
-    return r < b.ngroups ? r : b.ngroups;
-  };
-  bool bad = g.spg > kFlatMaxSpg;
-  const uint64_t stride = (uint64_t)gridDim.x * kFlatPrepBlock;
-  for (uint64_t p = (uint64_t)blockIdx.x * kFlatPrepBlock + threadIdx.x; p < b.count; p += stride) {
-    const uint64_t ps = b.offsets[p];
-    const uint32_t len = b.lengths[p];
-    const uint64_t pe = ps + len;
-    const uint64_t prev_end = p > 0 ? b.offsets[p - 1] + b.lengths[p - 1] : 0;
-    bool ok = len < kFlatMaxLen && (p == 0 || (ps >= prev_end && ps - prev_end <= kFlatMaxGap));
-    const uint64_t rlo = p > 0 ? region_ceil(prev_end) : 0, rhi = region_ceil(pe);
-    ok = ok && (rhi <= rlo || rhi - rlo <= kFlatMaxRegionsPerPacket);
-    if (ok)
-      for (uint64_t r = rlo; r < rhi; ++r) b.first[r] = (uint32_t)p;
-    bad = bad || !ok;
-  }
-  // Regions after the last packet's end: no packet.
-  const uint64_t rend = region_ceil(b.offsets[b.count - 1] + b.lengths[b.count - 1]);
-  for (uint64_t r = rend + (uint64_t)blockIdx.x * kFlatPrepBlock + threadIdx.x; r < b.ngroups; r += stride)
-    b.first[r] = (uint32_t)b.count;
-  bad = __syncthreads_or(bad);
-  if (threadIdx.x == 0) b.flags[blockIdx.x] = bad ? 1u : 0u;
-}
-
-struct FlatLds {
-  uint32_t tables[kLdsDwords];
-  u32x4 ring[kFlatRing][kWavesPerBlock][64];
-  uint32_t desc[kWavesPerBlock][2][2][64];  // [wave][window][offset low word | length][8 * group + i]
-};
-static_assert(sizeof(FlatLds) <= 160 * 1024, "LDS");
-
-// XOR of 4 LDS dwords and w, the reads hidden from hipcc (which would otherwise drain
-// every LDS-DMA in flight, vmcnt(0), before each table lookup it cannot tell from the
-// DMA destinations).
-__device__ __forceinline__ uint32_t lds_xor4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t w) {
-  asm volatile(
-      "ds_read_b32 %0, %0\n\t"
-      "ds_read_b32 %1, %1\n\t"
-      "ds_read_b32 %2, %2\n\t"
-      "ds_read_b32 %3, %3\n\t"
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t"
-      "v_bitop3_b32 %0, %0, %3, %4 bitop3:0x96"
-      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
-      : "v"(w)
-      : "memory");
-  return a0;
-}
-
-__device__ __forceinline__ uint32_t apply_rep_asm(uint32_t h, uint32_t w, uint32_t lp, const Lookup& lk) {
-  return lds_xor4(lookup_addr(h, lp, lk, 0), lookup_addr(h, lp, lk, 1), lookup_addr(h, lp, lk, 2),
-                  lookup_addr(h, lp, lk, 3), w);
-}
-
-// M32^n(x) through an unreplicated 4 x 256 table set at LDS byte address `set`.
-__device__ __forceinline__ uint32_t apply_small_asm(uint32_t set, uint32_t x) {
-  return lds_xor4(set + 4u * (x & 0xffu), set + 1024u + 4u * ((x >> 8) & 0xffu), set + 2048u + 4u * ((x >> 16) & 0xffu),
-                  set + 3072u + 4u * (x >> 24), 0u);
-}
-
-// combine_streams with every LDS read in asm (same arithmetic; tables at LDS address 0).
-__device__ __forceinline__ uint32_t combine_streams_asm(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
-                                                        const Lookup& lk) {
-  uint32_t y = apply_rep_asm(h0, h1, lk.lp1, lk);
-  y = apply_rep_asm(y, h2, lk.lp1, lk);
-  y = apply_rep_asm(y, h3, lk.lp1, lk);
-  const uint32_t k = threadIdx.x & (G - 1);
-  constexpr uint32_t tree = 4u * kTreeDword;
-  uint32_t t = 0;
-  if (k & 1u) t = apply_small_asm(tree, y);
-  y ^= from_lane_plus<1>(t);
-  if ((k & 3u) == 2u) t = apply_small_asm(tree + 4096u, y);
-  y ^= from_lane_plus<2>(t);
-  if (k == 4u) t = apply_small_asm(tree + 8192u, y);
-  y ^= from_lane_plus<4>(t);
-  return apply_rep_asm(y, 0u, lk.lp1, lk);
-}
-
-__global__ __launch_bounds__(kBlock) void crc32_flat_kernel(FlatBatch b, Batch<true> sb, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) FlatLds S;
-  const bool ok = flat_batch_ok(b);
-  fill_lds(S.tables);
-  __syncthreads();
-  if (!ok) {  // not flat-eligible: the streaming kernel's rounds (same grid, same tables)
-    stream_rounds<kStreamDepth, true>(S.tables, sb, out);
-    return;
-  }
-  if ((uint32_t)(uintptr_t)(LdsVoid*)S.tables != 0) __builtin_trap();  // horner_step_and_read addresses
-  const FlatGeo g = flat_geo(b);
-  const LaneConsts c = lane_consts(b.base);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t region = (blockIdx.x * kWavesPerBlock + wv) * kPacketsPerWave + c.grp;
-  const uint64_t r0 = g.lo + (uint64_t)region * g.rb;  // absolute start of this group's region
-  const uint64_t hi = g.lo + g.nsteps * 128u;
-  const uint32_t spg = (uint32_t)(g.rb >> 7);
-  const int32_t c0 = 112 - 16 * (int32_t)c.k;  // this lane's chunk inside a step
-  const uint32_t r0_lo = (uint32_t)r0, base_lo = (uint32_t)b.base;
-
-  // Data ring (as crc32_uniform_dma_kernel): DMA of step s lands in slot s % kFlatRing.
-  LdsVoid* const slot0 = (LdsVoid*)&S.ring[0][wv][0];
-  const uint32_t ring0 = (uint32_t)(uintptr_t)slot0;
-  uint32_t q = 0;
-  // Steps of this region that hold stream bytes (the last regions may reach past hi).
-  const uint32_t valid_steps = r0 >= hi ? 0u : (uint32_t)min((uint64_t)spg, (hi - r0) >> 7);
-  const uint64_t src0 = r0 + (uint64_t)c0;
-  auto dma_step = [&](uint32_t s) {
-    const uint64_t src = s < valid_steps ? src0 + 128ull * s : c.dummy;
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 0);
-    q = q + 1 == (uint32_t)kFlatRing ? 0u : q + 1;
-  };
-  // Descriptor windows: lane 8g+i of window w holds packet wbase + i of group g.  The
-  // DMAs are asm with their own M0: groups of one wave refill different windows in the
-  // same iteration, and hipcc merges two builtin calls into one whose M0 is the first
-  // active lane's window (readfirstlane), which overwrites other groups' windows.
-  auto dma_desc = [&](auto w_const, uint32_t first_packet) {
-    constexpr uint32_t w = decltype(w_const)::value;
-    uint64_t p = (uint64_t)first_packet + c.k;
-    p = p < b.count ? p : b.count - 1;
-    const uint64_t src_off = (uint64_t)(uintptr_t)(b.offsets + p), src_len = (uint64_t)(uintptr_t)(b.lengths + p);
-    const uint32_t m_off = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LdsVoid*)&S.desc[wv][w][0][0]);
-    const uint32_t m_len = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LdsVoid*)&S.desc[wv][w][1][0]);
-    uint32_t saved_m0;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "global_load_lds_dword %1, off\n\t"
-        "s_mov_b32 m0, %4\n\t"
-        "global_load_lds_dword %2, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved_m0)
-        : "v"(src_off), "v"(src_len), "s"(m_off), "s"(m_len)
-        : "memory");
-  };
-  const uint32_t desc_lds = (uint32_t)(uintptr_t)(LdsVoid*)&S.desc[wv][0][0][0] + 4u * kLanesPerPacket * c.grp;
-  uint32_t p = region == 0 ? 0u : b.first[region];  // region 0 also takes empty packets at lo
-  auto read_desc = [&](uint32_t pk, uint32_t w, uint32_t i, int32_t& ps, int32_t& pe) {  // packet pk: window w, entry i
-    uint32_t olo, len;
-    const uint32_t a = desc_lds + 512u * w + 4u * i;
-    asm volatile(
-        "ds_read_b32 %0, %2\n\t"
-        "ds_read_b32 %1, %2 offset:256\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(olo), "=&v"(len)
-        : "v"(a)
-        : "memory");
-    const bool valid = pk < b.count;
-    ps = valid ? (int32_t)(olo + base_lo - r0_lo) : kFlatFar;
-    pe = valid ? ps + (int32_t)len : kFlatFar;
-  };
-
-  uint32_t wbase = p, cw = 0, win_ready = 0;
-  dma_desc(std::integral_constant<uint32_t, 0>{}, wbase);
-  dma_desc(std::integral_constant<uint32_t, 1>{}, wbase + 8u);
-  __builtin_amdgcn_s_waitcnt(0);  // prologue: both windows landed (vmcnt 0)
-  int32_t ps, pe;
-  read_desc(p, 0, 0, ps, pe);
-  // Next boundary: this packet's start if it lies inside the region (after a gap),
-  // else its end.
-  bool start_pending = ps > 0 && ps < kFlatFar;
-  int32_t xn = start_pending ? ps : pe;
-#pragma unroll
-  for (int f = 0; f < kFlatRing; ++f) dma_step((uint32_t)f);
-  u32x4 nextv = read_landed_slot<kFlatRing - 1>(ring0 + lane * 16u);
-
-  // Boundary values wait in one park slot per group (4 stream words per lane and the
-  // destination) and are combined for all groups at once when some group needs the slot
-  // again: one combine pass serves several groups instead of one pass per boundary.
-  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-  uint32_t pv0 = 0, pv1 = 0, pv2 = 0, pv3 = 0;
-  uint32_t pidx = 0, pkind = 0;  // parked value's packet and kind (0: slot empty, 1: end, 2: start)
-  auto flush = [&]() {           // wave-uniform call
-    const uint32_t E = combine_streams_asm(pv0, pv1, pv2, pv3, c.lk);  // lane k == 0
-    if (pkind != 0u && c.k == 0) (pkind == 2u ? b.e_start : b.e_end)[pidx] = E;
-    pkind = 0;
-  };
-  // Stream bytes at and after a boundary: word j of this lane keeps bytes >= the boundary,
-  // (uint32_t)(~0 << clamp(8 * (x - 4j), 0, 32)) with x the boundary's byte in my chunk.
-  auto above = [](int32_t x8, int32_t j) -> uint32_t {
-    const uint32_t n = (uint32_t)min(max(x8 - 32 * j, 0), 32);
-    return (uint32_t)(~0ull << n);
-  };
-  for (uint32_t s = 0; s < spg; ++s) {
-    const u32x4 v = nextv;
-    dma_step(s + kFlatRing);
-    const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
-    uint32_t x0 = h0, x1 = h1, x2 = h2, x3 = h3;  // -> M32^32(h) ^ w
-    horner_step_and_read<kFlatRing - 1>(c.lk, x0, x1, x2, x3, v.x, v.y, v.z, v.w, next_addr, nextv);
-    issue_order_fence();
-    h0 = x0;
-    h1 = x1;
-    h2 = x2;
-    h3 = x3;
-    const int32_t S0 = 128 * (int32_t)s;
-    // Boundaries in (S0, S0 + 128]: park the streams without this step's bytes >= x.
-    // One boundary per group per pass; the state updates are selects (no divergent
-    // branches but the rare window switch).
-    while (__builtin_amdgcn_ballot_w64(xn <= S0 + 128)) {
-      const bool act = xn <= S0 + 128;
-      if (__builtin_amdgcn_ballot_w64(act && pkind != 0u)) flush();
-      const int32_t x8 = 8 * (xn - S0 - c0);
-      const uint32_t n0 = x0 ^ (v.x & above(x8, 0)), n1 = x1 ^ (v.y & above(x8, 1));
-      const uint32_t n2 = x2 ^ (v.z & above(x8, 2)), n3 = x3 ^ (v.w & above(x8, 3));
-      pv0 = act ? n0 : pv0;
-      pv1 = act ? n1 : pv1;
-      pv2 = act ? n2 : pv2;
-      pv3 = act ? n3 : pv3;
-      pidx = act ? p : pidx;
-      pkind = act ? (start_pending ? 2u : 1u) : pkind;
-      const bool is_end = act && !start_pending;  // a start boundary is followed by its packet's end
-      const uint32_t np = p + (is_end ? 1u : 0u);
-      if (__builtin_amdgcn_ballot_w64(np - wbase == 8u)) {  // a window used up: switch, refill the other
-        if (s < win_ready) __builtin_amdgcn_s_waitcnt(0);    // the other window's DMA may be in flight
-        if (np - wbase == 8u) {
-          wbase += 8u;
-          cw ^= 1u;
-          if (cw == 1u) dma_desc(std::integral_constant<uint32_t, 0>{}, wbase + 8u);
-          if (cw == 0u) dma_desc(std::integral_constant<uint32_t, 1>{}, wbase + 8u);
-        }
-        win_ready = s + (uint32_t)kFlatRing + 1u;
-      }
-      p = np;
-      int32_t nps, npe;
-      read_desc(p, cw, p - wbase, nps, npe);  // used by the lanes that just passed an end
-      const bool gap = nps != pe && nps < kFlatFar;
-      xn = is_end ? (gap ? nps : npe) : (act ? pe : xn);
-      start_pending = is_end ? gap : (act ? false : start_pending);
-      pe = is_end ? npe : pe;
-    }
-  }
-  if (__builtin_amdgcn_ballot_w64(pkind != 0u)) flush();
-  {
-    const uint32_t t = combine_streams_asm(h0, h1, h2, h3, c.lk);  // G_r(R1)
-    if (c.k == 0) b.tails[region] = t;
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // the ring's last DMAs land before the wave's LDS goes away
-}
-
-// One thread per packet turns the boundary values into checksums (eligible batches; the
-// main kernel ran the fallback rounds otherwise).
-__global__ __launch_bounds__(kBlock) void crc32_flat_finish_kernel(FlatBatch b, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[(kFinFwdLds + kInvLevels) * kSlotLevelDwords + 256 + 64];
-  if (!flat_batch_ok(b)) return;
-  // LDS: forward levels 5..5+kFinFwdLds-1, kInvLevels inverse levels, CRC table, inv_top.
-  uint32_t* const fwd = lds;
-  uint32_t* const inv = lds + kFinFwdLds * kSlotLevelDwords;
-  uint32_t* const crc_table = inv + kInvLevels * kSlotLevelDwords;
-  uint8_t* const inv_top = reinterpret_cast<uint8_t*>(crc_table + 256);
-  const uint32_t* inv_g = b.ladder + kSlotLevels * kSlotLevelDwords;
-  const uint32_t* init_tab = inv_g + kInvLevels * kSlotLevelDwords;
-  {  // every load issued before the first store (one memory latency, not one per level)
-    static_assert(kSlotLevelDwords == kBlock, "one dword per thread per level");
-    uint32_t f[kFinFwdLds], iv[kInvLevels];
-#pragma unroll
-    for (int i = 0; i < kFinFwdLds; ++i) f[i] = b.ladder[(kFinFwdBase + i) * kSlotLevelDwords + threadIdx.x];
-#pragma unroll
-    for (int i = 0; i < kInvLevels; ++i) iv[i] = inv_g[i * kSlotLevelDwords + threadIdx.x];
-    const uint32_t ct = threadIdx.x < 256u ? g_op_tables.sarwate[threadIdx.x] : 0u;
-    const uint8_t it = threadIdx.x < 256u ? g_op_tables.inv_top[threadIdx.x] : 0u;
-#pragma unroll
-    for (int i = 0; i < kFinFwdLds; ++i) fwd[i * kSlotLevelDwords + threadIdx.x] = f[i];
-#pragma unroll
-    for (int i = 0; i < kInvLevels; ++i) inv[i * kSlotLevelDwords + threadIdx.x] = iv[i];
-    if (threadIdx.x < 256u) {
-      crc_table[threadIdx.x] = ct;
-      inv_top[threadIdx.x] = it;
-    }
-  }
-  __syncthreads();
-  const FlatGeo g = flat_geo(b);
-  // x -> M8^(128 m)(x) = M32^(32 m)(x): LDS levels first, global ones for large m.
-  auto fwd_steps = [&](uint32_t x, uint64_t m) {
-#pragma unroll
-    for (int i = 0; i < kFinFwdLds; ++i)
-      if ((m >> i) & 1u) x = ladder_apply(fwd + i * kSlotLevelDwords, x);
-    m >>= kFinFwdLds;
-    for (int i = kFinFwdLds; m != 0; ++i, m >>= 1)
-      if (m & 1u) x = ladder_apply(b.ladder + (kFinFwdBase + i) * kSlotLevelDwords, x);
-    return x;
-  };
-  // Region index of a boundary at absolute address x > lo: the region with R0 < x <= R1.
-  const bool small_span = g.nsteps * 128u < (1ull << 32);
-  const uint32_t rb32 = (uint32_t)g.rb;
-  auto region_of = [&](uint64_t x) -> uint64_t {
-    return small_span ? (uint64_t)((uint32_t)(x - g.lo - 1) / rb32) : (x - g.lo - 1) / g.rb;
-  };
-  // Inputs of one packet; the next packet's are loaded before this one is computed.
-  struct In {
-    uint64_t off, prev_end;
-    uint32_t len, ee, eprev, es, iv;
-  };
-  auto load_in = [&](uint64_t p, In& in) {
-    in.len = b.lengths[p];
-    in.off = b.offsets[p];
-    in.prev_end = p > 0 ? b.offsets[p - 1] + b.lengths[p - 1] : ~(uint64_t)0;
-    in.ee = b.e_end[p];
-    in.eprev = p > 0 ? b.e_end[p - 1] : 0u;
-    in.es = b.e_start[p];  // meaningful only after a gap
-    in.iv = init_tab[in.len < kInitTabLen ? in.len : 0u];
-  };
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  In nx{};
-  if (p < b.count) load_in(p, nx);
-  for (; p < b.count; p += stride) {
-    const In in = nx;
-    if (p + stride < b.count) load_in(p + stride, nx);
-    const uint64_t sa = b.base + in.off, ea = sa + in.len;
-    if (ea <= g.lo) {  // an empty packet at lo
-      out[p] = 0u;
-      continue;
-    }
-    const uint64_t te = (ea + 127u) & ~(uint64_t)127;  // end of the step holding the end boundary
-    uint32_t reg = in.ee;
-    // Tails of the regions from the one holding the start boundary to the one before the end's.
-    const uint64_t rs = sa > g.lo ? region_of(sa) : 0, re = region_of(ea);
-    for (uint64_t r = rs; r < re; ++r) reg ^= fwd_steps(b.tails[r], (te - (g.lo + (r + 1) * g.rb)) >> 7);
-    if (sa > g.lo) {  // E(start): the previous packet's end value when they touch
-      const uint32_t es = b.base + in.prev_end == sa ? in.eprev : in.es;
-      reg ^= fwd_steps(es, (te - ((sa + 127u) & ~(uint64_t)127)) >> 7);
-    }
-    // M8^-(te - ea): < 32 words through the inverse levels, then < 4 bytes.
-    const uint32_t u = (uint32_t)(te - ea);
-    uint32_t wq = u >> 2;
-    for (int k = 0; wq != 0; ++k, wq >>= 1)
-      if (wq & 1u) reg = ladder_apply(inv + k * kSlotLevelDwords, reg);
-    for (uint32_t t = 0; t < (u & 3u); ++t) {
-      const uint32_t idx = inv_top[reg >> 24];
-      reg = ((reg ^ crc_table[idx]) << 8) | idx;
-    }
-    // Initial register: M8^len(0xFFFFFFFF).
-    uint32_t iv = in.iv;
-    if (in.len >= kInitTabLen) {
-      iv = kInitRegister;
-      for (uint32_t t = 0; t < (in.len & 3u); ++t) iv = (iv >> 8) ^ crc_table[iv & 0xffu];
-      uint32_t m = in.len >> 2;
-      for (int k = 0; m != 0; ++k, m >>= 1)
-        if (m & 1u) iv = ladder_apply(b.ladder + k * kSlotLevelDwords, iv);
-    }
-    out[p] = __builtin_bswap32(~(reg ^ iv));
-  }
-}
 
 }  // namespace
 
@@ -2434,49 +1563,17 @@ static unsigned grid_for(uint64_t count, hipError_t& err) {
   return (unsigned)blocks;
 }
 
-// ENET_CRC_SPLIT=0: piece loads instead of line-split loads (A/B runs).  Read per launch.
-static bool use_split_loads() {
-  const char* v = getenv("ENET_CRC_SPLIT");
-  return !(v && strcmp(v, "0") == 0);
-}
-
 template <int NS>
 static hipError_t launch_uniform_regs(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
-  if (use_split_loads())
-    hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS, true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
-  else
-    hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS, false>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
 
-template <int NS>
-static hipError_t launch_uniform_dma(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
-  hipLaunchKernelGGL((crc32_uniform_dma_kernel<NS>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
-  return hipGetLastError();
-}
-
-// Long packets that all end on a 128-B line (e.g. 64 KiB buffers from an aligned base):
-// the runtime-step kernel with non-temporal DMAs.  ENET_CRC_NT=0 turns the hint off
-// (A/B runs).  Read per launch.
+// Packets that all end on a 128-B line (e.g. 64 KiB buffers from an aligned base): the
+// DMAs carry the non-temporal hint (every group slot is one whole line of its own).
 static bool nt_lines(const UniformBatch& u) {
-  const char* v = getenv("ENET_CRC_NT");
-  if (v && strcmp(v, "0") == 0) return false;
   const uint64_t lx = (u.length + 3u) & ~3u;
   return ((u.base + lx) & 127u) == 0 && (u.stride & 127u) == 0;
-}
-
-// ns in 1..kMaxRoundSteps: the unrolled kernel; longer: the runtime-step kernel (NS = 0).
-template <int... I>
-static hipError_t dispatch_uniform_dma(int ns, const UniformBatch& u, uint32_t* out, hipStream_t stream,
-                                       unsigned blocks, std::integer_sequence<int, I...>) {
-  hipError_t e = hipErrorInvalidValue;
-  const bool hit = ((ns == I + 1 ? (e = launch_uniform_dma<I + 1>(u, out, stream, blocks), true) : false) || ...);
-  if (hit) return e;
-  if (nt_lines(u)) {
-    hipLaunchKernelGGL((crc32_uniform_dma_kernel<0, true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
-    return hipGetLastError();
-  }
-  return launch_uniform_dma<0>(u, out, stream, blocks);
 }
 
 // ns in 1..kMaxRoundSteps only (the register ring holds a whole round).
@@ -2488,15 +1585,10 @@ static hipError_t dispatch_uniform_regs(int ns, const UniformBatch& u, uint32_t*
   return e;
 }
 
-// Aligned uniform batches of packets up to kMaxRoundSteps steps (≤ 1792 B) run the
-// register-ring kernel, longer ones the LDS-DMA kernel.  Every alternating A/B so far
-// had the register ring 1-3 % ahead on G1; ENET_CRC_UNIFORM=dma selects
-// the LDS-DMA kernel for all lengths (A/B runs).  Read per launch.
-static bool use_regs_uniform() {
-  const char* v = getenv("ENET_CRC_UNIFORM");
-  return !(v && strcmp(v, "dma") == 0);
-}
-
+// Aligned uniform batches (base and stride multiples of 4): packets up to kMaxRoundSteps
+// steps (<= 1792 B) run the register ring with line-split loads (the G1 path), packets of
+// >= 4 KiB the wave-per-packet kernel, the lengths in between the 8-packets-per-wave
+// LDS-DMA kernel.  Unaligned uniform batches: the round kernels of the register form.
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
                           uint32_t* out, hipStream_t stream) {
   if (count == 0) return hipSuccess;
@@ -2507,14 +1599,10 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
     const int nsx = make_geo(0, (length + 3u) & ~3u).nsteps;
     const unsigned blocks = grid_for(count, err);
     if (err != hipSuccess) return err;
-    UniformBatch u{b0, stride, length, count};
-    const char* xv = getenv("ENET_CRC_XCD");
-    u.xcd_swizzle = (xv && strcmp(xv, "1") == 0) ? 1u : 0u;
-    // Packets of >= 4 KiB: the wave-per-packet kernel (1-KiB contiguous loads); 64-KiB
-    // buffers 338-346 us vs 371-374 us for the 8-packets-per-wave DMA kernel, 3 alternating
-    // pairs.  ENET_CRC_LONG=group restores the latter (A/B runs).
-    const char* lv = getenv("ENET_CRC_LONG");
-    if (!(lv && strcmp(lv, "group") == 0) && length >= (uint32_t)kWaveRing * kWaveStep) {
+    const UniformBatch u{b0, stride, length, count};
+    // Packets of >= 4 KiB: one wave per packet, 1-KiB contiguous loads; 64-KiB buffers
+    // 338-346 us vs 371-374 us for the 8-packets-per-wave DMA kernel.
+    if (length >= (uint32_t)kWaveRing * kWaveStep) {
       uint64_t wblocks = (count + kWavesPerBlock - 1) / kWavesPerBlock;
       const int cus = cu_count_for_current_device();
       if (wblocks > (uint64_t)cus) wblocks = (uint64_t)cus;
@@ -2524,9 +1612,13 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
         hipLaunchKernelGGL((crc32_wave_dma_kernel<false>), dim3((unsigned)wblocks), dim3(kBlock), 0, stream, u, out);
       return hipGetLastError();
     }
-    if (use_regs_uniform() && nsx <= kMaxRoundSteps)
+    if (nsx <= kMaxRoundSteps)
       return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
-    return dispatch_uniform_dma(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
+    if (nt_lines(u))
+      hipLaunchKernelGGL((crc32_uniform_dma_kernel<true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+    else
+      hipLaunchKernelGGL((crc32_uniform_dma_kernel<false>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+    return hipGetLastError();
   }
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
@@ -2657,117 +1749,30 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const unsigned blocks = grid_for(count, err);
   if (err != hipSuccess) return err;
   Batch<true> b{(uint64_t)(uintptr_t)base, offsets, lengths, 0, 0, count};
-  // Default: regions of the batch sorted by step class (region records kernel), then
-  // the round DMA kernel.  ENET_CRC_RAGGED=flat: the flat-stream kernels (prep, main,
-  // finish; the finish launch runs the streaming kernel's rounds for a batch the prep
-  // kernel refused); =flatonly the same WITHOUT the fallback rounds (tests and A/B runs
-  // on batches known to be in address order; any other batch leaves `out` undefined);
-  // =groups the group-stream kernel (no pre-pass; bit-exact, but 1.28x slower on G2:
-  // DESIGN.md §4); =stream the streaming kernel after the sort.
-  // (Read per launch, not cached, so one process can A/B and test every path.)
-  const int ragged_mode = [] {
-    const char* v = getenv("ENET_CRC_RAGGED");
-    if (v && strcmp(v, "stream") == 0) return 2;
-    if (v && strcmp(v, "groups") == 0) return 0;
-    if (v && strcmp(v, "flat") == 0) return 3;
-    if (v && strcmp(v, "flatonly") == 0) return 4;
-    return 1;
-  }();
-  if (count > 0xFFFFFFFFull || (ragged_mode != 0 && count < kSortMinPackets)) {
+  if (count > 0xFFFFFFFFull || count < kSortMinPackets) {
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  if (ragged_mode == 0) {
-    const uint64_t ntasks = (count + kGsTask - 1) / kGsTask;
-    uint64_t gblocks = (ntasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (gblocks > (uint64_t)blocks) gblocks = blocks;
-    const GsBatch gb{b.base, offsets, lengths, count};
-    hipLaunchKernelGGL(crc32_group_stream_kernel, dim3((unsigned)gblocks), dim3(kBlock), 0, stream, gb, out);
-    return hipGetLastError();
-  }
-  if (ragged_mode == 3 || ragged_mode == 4) {
-    // Flat path: prep, main, finish (whose blocks run the streaming kernel's rounds
-    // instead when the prep kernel refused the batch).  Regions = groups of the main
-    // kernel's grid (128 per workgroup, at most one workgroup per CU, about two packets
-    // per group at least).
-    uint64_t ngroups = ((count / 2 + 127) / 128) * 128;
-    const uint64_t max_groups = (uint64_t)blocks * kWavesPerBlock * kPacketsPerWave;
-    ngroups = ngroups < 128 ? 128 : (ngroups > max_groups ? max_groups : ngroups);
-    uint64_t nflags = (count + kFlatPrepBlock - 1) / kFlatPrepBlock;
-    nflags = nflags < kFlatMaxFlags ? nflags : kFlatMaxFlags;
-    const uint32_t* ladder = nullptr;
-    err = device_slot_ladder(&ladder);
-    if (err != hipSuccess) return err;
-    void* scratch = nullptr;
-    hipMemPool_t pool = nullptr;
-    err = scratch_pool(&pool);
-    if (err != hipSuccess) return err;
-    const size_t words = (size_t)kFlatMaxFlags + 2 * ngroups + 2 * count;
-    err = hipMallocFromPoolAsync(&scratch, words * 4, pool, stream);
-    if (err != hipSuccess) return err;
-    uint32_t* fs = static_cast<uint32_t*>(scratch);
-    const FlatBatch fb{b.base, offsets, lengths, count, (uint32_t)ngroups, (uint32_t)nflags, fs,
-                       fs + kFlatMaxFlags, fs + kFlatMaxFlags + ngroups, fs + kFlatMaxFlags + 2 * ngroups,
-                       fs + kFlatMaxFlags + 2 * ngroups + count, ladder};
-    Batch<true> sb = b;
-    if (ragged_mode == 4) sb.count = 0;  // ENET_CRC_RAGGED=flatonly: no fallback rounds
-    hipLaunchKernelGGL(crc32_flat_prep_kernel, dim3((unsigned)nflags), dim3(kFlatPrepBlock), 0, stream, fb);
-    hipLaunchKernelGGL(crc32_flat_kernel, dim3((unsigned)(ngroups / 128)), dim3(kBlock), 0, stream, fb, sb, out);
-    uint64_t fin_blocks = (count + kBlock - 1) / kBlock;
-    fin_blocks = fin_blocks < 2ull * blocks ? fin_blocks : 2ull * blocks;
-    hipLaunchKernelGGL(crc32_flat_finish_kernel, dim3((unsigned)fin_blocks), dim3(kBlock), 0, stream, fb, out);
-    err = hipGetLastError();
-    const hipError_t ferr = hipFreeAsync(scratch, stream);
-    return err != hipSuccess ? err : ferr;
-  }
-  if (ragged_mode == 1) {
-    // Region records + the round DMA kernel with XCD-aligned rounds (grid multiple of 8).
-    const bool xcd = blocks % 8 == 0 && (uint64_t)blocks * kWavesPerBlock <= kRegionMax;
-    const uint32_t region = xcd ? blocks * kWavesPerBlock : kRegionMax;
-    const uint64_t nregions = (count + region - 1) / region;
-    const uint64_t rounds = (count + kPacketsPerWave - 1) / kPacketsPerWave;
-    void* scratch = nullptr;
-    hipMemPool_t pool = nullptr;
-    err = scratch_pool(&pool);
-    if (err != hipSuccess) return err;
-    bool owned = true;
-    std::unique_lock<std::mutex> held;  // until both launches are enqueued
-    err = records_scratch(stream, (size_t)rounds * kRecordBytes, pool, &scratch, &owned, held);
-    if (err != hipSuccess) return err;
-    uint8_t* recs = static_cast<uint8_t*>(scratch);
-    hipLaunchKernelGGL(crc32_region_records_kernel, dim3((unsigned)nregions), dim3(kRegionBlock), 0, stream, b,
-                       region, recs);
-    const char* ft = getenv("ENET_CRC_FASTTOP");
-    const RaggedDmaBatch rb{b.base, recs, count, xcd ? 1u : 0u, (ft && strcmp(ft, "0") == 0) ? 1u : 0u};
-    hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
-    err = hipGetLastError();
-    const hipError_t ferr = owned ? hipFreeAsync(scratch, stream) : hipSuccess;
-    return err != hipSuccess ? err : ferr;
-  }
-  // ENET_CRC_RAGGED=stream: the whole batch sorted by class (histogram + scatter), then
-  // the streaming kernel through the permutation.
-  // >= 4096 packets per sort block: every records/scatter block reads the whole
-  // histogram (16 x sort_blocks entries) to find its output positions.
-  uint64_t sort_blocks = (count + 16 * kSortBlock - 1) / (16 * kSortBlock);
-  sort_blocks = sort_blocks < 1024 ? sort_blocks : 1024;
-  const size_t hist_bytes = ((size_t)kStepClasses * sort_blocks * 4 + 255) & ~(size_t)255;
-  const size_t tail_bytes = (size_t)count * 4;
+  // Region records + the round DMA kernel with XCD-aligned rounds (grid multiple of 8).
+  const bool xcd = blocks % 8 == 0 && (uint64_t)blocks * kWavesPerBlock <= kRegionMax;
+  const uint32_t region = xcd ? blocks * kWavesPerBlock : kRegionMax;
+  const uint64_t nregions = (count + region - 1) / region;
+  const uint64_t rounds = (count + kPacketsPerWave - 1) / kPacketsPerWave;
   void* scratch = nullptr;
   hipMemPool_t pool = nullptr;
   err = scratch_pool(&pool);
   if (err != hipSuccess) return err;
-  err = hipMallocFromPoolAsync(&scratch, hist_bytes + tail_bytes, pool, stream);
+  bool owned = true;
+  std::unique_lock<std::mutex> held;  // until both launches are enqueued
+  err = records_scratch(stream, (size_t)rounds * kRecordBytes, pool, &scratch, &owned, held);
   if (err != hipSuccess) return err;
-  uint32_t* hist = static_cast<uint32_t*>(scratch);
-  uint8_t* second = static_cast<uint8_t*>(scratch) + hist_bytes;
-  hipLaunchKernelGGL(crc32_class_hist_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b, hist);
-  uint32_t* perm = reinterpret_cast<uint32_t*>(second);
-  hipLaunchKernelGGL(crc32_class_scatter_kernel, dim3((unsigned)sort_blocks), dim3(kSortBlock), 0, stream, b,
-                     (const uint32_t*)hist, perm);
-  b.perm = perm;
-  Launcher<true> L{b, out, stream, blocks};
-  err = L.streaming();
-  const hipError_t ferr = hipFreeAsync(scratch, stream);
+  uint8_t* recs = static_cast<uint8_t*>(scratch);
+  hipLaunchKernelGGL(crc32_region_records_kernel, dim3((unsigned)nregions), dim3(kRegionBlock), 0, stream, b,
+                     region, recs);
+  const RaggedDmaBatch rb{b.base, recs, count, xcd ? 1u : 0u};
+  hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
+  err = hipGetLastError();
+  const hipError_t ferr = owned ? hipFreeAsync(scratch, stream) : hipSuccess;
   return err != hipSuccess ? err : ferr;
 }
 

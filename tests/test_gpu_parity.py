@@ -232,27 +232,6 @@ def test_per_call_65_slices(dev):
         assert rea.crc32(slices) == _oracle.crc32(slices)
 
 
-# --- the alternative ragged kernels (ENET_CRC_RAGGED), same oracle --------------------------
-
-@pytest.mark.parametrize("mode", ["groups", "stream"])
-def test_alternative_ragged_kernels(dev, mode, monkeypatch):
-    monkeypatch.setenv("ENET_CRC_RAGGED", mode)
-    lens, offs, pos = [], [], 0
-    for n in range(0, 300):
-        for a in range(8):
-            pos += a
-            offs.append(pos)
-            lens.append(n)
-            pos += n
-    data = splitmix64_bytes(12, pos + 64)
-    offsets, lengths = np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
-    assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
-    lengths = ragged_lengths(ENET_SEED + 5, 200_000, lo=0, hi=4096)
-    offsets = packed_offsets(lengths) + np.uint64(1)
-    data = splitmix64_bytes(13, int(lengths.sum()) + 8)
-    assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
-
-
 # --- region sort (default ragged pre-pass): region sizes and grids around its edges ----------
 
 @pytest.mark.parametrize("count", [4096, 4100, 5000, 8 * 4096 + 3, 70_001])
@@ -272,13 +251,10 @@ def test_ragged_region_sort_edges(dev, count):
 
 # --- round-record scratch cached per stream (launch_ragged) ----------------------------------
 
-@pytest.mark.parametrize("cache", ["default", "0"])
-def test_ragged_scratch_per_stream(dev, cache, monkeypatch):
+def test_ragged_scratch_per_stream(dev):
     # Two streams, each launching sorted ragged batches that grow (the cached buffer is
     # regrown stream-ordered) and shrink (reused), interleaved without synchronising in
-    # between; every result is kept and checked afterwards.  cache "0": allocate per launch.
-    if cache != "default":
-        monkeypatch.setenv("ENET_CRC_SCRATCH_CACHE", cache)
+    # between; every result is kept and checked afterwards.
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     jobs = []
     for i, count in enumerate([5000, 40_000, 9000, 120_000, 4096, 70_000]):
@@ -299,14 +275,11 @@ def test_ragged_scratch_per_stream(dev, cache, monkeypatch):
 
 # --- whole-line loads: line-split register ring, non-temporal long packets -----------------
 
-@pytest.mark.parametrize("split", ["default", "0"])
 @pytest.mark.parametrize("base_off", [0, 4, 12, 16, 48, 100, 124])
-def test_uniform_line_split_bases(dev, split, base_off, monkeypatch):
+def test_uniform_line_split_bases(dev, base_off):
     # Packet ends at every 16-B residue mod 128 (lo = 0..7 lanes taking entry s + 1),
     # lengths that are and are not multiples of 16, the first packets within a chunk of
     # the base (fallback loads), and a batch that ends exactly at the buffer's end.
-    if split != "default":
-        monkeypatch.setenv("ENET_CRC_SPLIT", split)
     for stride, length, n in [(1200, 1200, 3001), (1392, 1392, 2999), (1204, 1200, 2048), (16, 16, 5000),
                               (132, 128, 4000), (1796, 1792, 1500), (400, 396, 3333)]:
         data = splitmix64_bytes(base_off * 7 + stride + length, base_off + (n - 1) * stride + length)
@@ -316,15 +289,15 @@ def test_uniform_line_split_bases(dev, split, base_off, monkeypatch):
         assert np.array_equal(got, want), (stride, length, base_off)
 
 
-@pytest.mark.parametrize("nt", ["default", "0"])
-def test_long_packets_line_ends(dev, nt, monkeypatch):
+def test_long_packets_line_ends(dev):
     # Non-temporal DMAs need every packet to end on a 128-B line: ends aligned with the
     # starts aligned (64 KiB from an aligned base) or not (65536 - 128 from base + 128),
     # and a base that breaks the line ends (the plain path).
-    if nt != "default":
-        monkeypatch.setenv("ENET_CRC_NT", nt)
+    # 1920 and 3968 B (15 and 31 steps): the 8-packets-per-wave DMA kernel, with and
+    # without the hint; 2000 B from base + 4: that kernel without it.
     for base_off, stride, length, n in [(0, 65536, 65536, 64), (128, 65536, 65408, 64), (4, 65536, 65536, 48),
-                                        (256, 8192, 4096, 300)]:
+                                        (256, 8192, 4096, 300), (0, 1920, 1920, 5000), (0, 3968, 3968, 1000),
+                                        (4, 1920, 1920, 4000), (4, 2000, 2000, 3000), (0, 4092, 4090, 999)]:
         data = splitmix64_bytes(base_off + length, base_off + (n - 1) * stride + length)
         d = to_dev(data, dev)[base_off:]
         got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
@@ -332,16 +305,12 @@ def test_long_packets_line_ends(dev, nt, monkeypatch):
         assert np.array_equal(got, want), (base_off, stride, length)
 
 
-@pytest.mark.parametrize("long_mode", ["default", "group"])
 @pytest.mark.parametrize("base_off", [0, 4, 12, 128, 1000])
-def test_long_packets_wave_kernel(dev, long_mode, base_off, monkeypatch):
-    # Default: one wave per packet, 1-KiB steps (crc32_wave_dma_kernel); ENET_CRC_LONG=group:
-    # 8 packets per wave (crc32_uniform_dma_kernel<0>).
+def test_long_packets_wave_kernel(dev, base_off):
+    # One wave per packet, 1-KiB steps (crc32_wave_dma_kernel).
     # Lengths from the 4-KiB minimum up, multiples of 1 KiB and 128 B or not, odd lengths
     # (bytes past the end masked), gaps between packets, packets within a chunk of the
     # base (fallback loads), counts that are not multiples of the wave count.
-    if long_mode != "default":
-        monkeypatch.setenv("ENET_CRC_LONG", long_mode)
     for stride, length, n in [(65536, 65536, 200), (4096, 4096, 3001), (4100, 4097, 999), (5000, 4999, 777),
                               (12288, 10001, 300), (65540, 65537, 33), (70000, 65536, 17), (8192, 8191, 1),
                               (4096, 4096, 4097)]:
@@ -349,21 +318,7 @@ def test_long_packets_wave_kernel(dev, long_mode, base_off, monkeypatch):
         d = to_dev(data, dev)[base_off:]
         got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
         want = _oracle.crc32_uniform(data[base_off:], stride, length, n, threads=8)
-        assert np.array_equal(got, want), (long_mode, stride, length, n, base_off)
-
-
-def test_full_shard_large_group_kernel(dev, monkeypatch):
-    # The G4 per-GPU shard (32,768 x 64 KiB) through the 8-packets-per-wave kernel
-    # (ENET_CRC_LONG=group; the default path is test_full_shard_large_32768_x_64k).
-    monkeypatch.setenv("ENET_CRC_LONG", "group")
-    n, L = 32768, 65536
-    g = torch.Generator(device=dev)
-    g.manual_seed(ENET_SEED + 5)
-    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
-    got = as_u32(rea.crc32_batch(d, stride=L, length=L, count=n))
-    want = _oracle.crc32_uniform(d.cpu().numpy(), L, L, n, threads=16)
-    del d
-    assert np.array_equal(got, want)
+        assert np.array_equal(got, want), (stride, length, n, base_off)
 
 
 def test_long_packets_random_layouts(dev):
