@@ -27,3 +27,12 @@ clean:
 
 $(ORACLE_RANGE): oracle/range_coder_oracle.c
 	$(CC) -O2 -fPIC -shared -Wall -o $@ $<
+
+# A/B builds of the library with compile-time variant switches (never the product):
+#   make variant NAME=region DEFS=-DENET_CRC_REGION_RAGGED
+#   -> rusty_enet_amd/lib/variants/libenet_crc_amd_region.so, loaded with ENET_CRC_AMD_LIB.
+variant: $(HIP_DEP)
+	mkdir -p rusty_enet_amd/lib/variants
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o rusty_enet_amd/lib/variants/libenet_crc_amd_$(NAME).so $(HIP_SRC)
+
+.PHONY: variant

@@ -53,6 +53,8 @@ CONFIGS = {
     "ragged": ("ragged packets, lengths U{64..1392}, packed at byte offsets; BASELINE configs[2]",
                1 << 20, 1 << 20),
     "large": ("64 KiB buffers, one CRC each (large-buffer path); BASELINE configs[4]", 32768, 32768),
+    "frag": ("64 KiB payloads fragmented at the default MTU (48 x 1392 B + 288 B datagrams each, one CRC per "
+             "datagram); the configs[4] bytes as the reference checksums them", 32768, 32768),
     "range": ("ragged compressible packets, lengths U{64..1392}, range-coder compress (SURVEY.md 8(f)4)",
               1 << 20, 1 << 20),
 }
@@ -505,6 +507,42 @@ def uniform_point(dev, rank: int, n: int, L: int, steps: int, warmup: int, barri
     return config_point("uniform", dev, rank, n, steps, warmup, barrier, length=L)
 
 
+def device_record(dev, rank: int) -> dict:
+    """Which physical GPU this rank ran on (gathered into the line's `devices` field)."""
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    return {"rank": rank, "device": dev.index, "name": p.name,
+            "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid)}
+
+
+def gather_objects(obj, world: int) -> list:
+    """obj from every rank (gloo), rank order; [obj] without a process group."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def all_ranks_point(name: str, dev, rank: int, world: int, n: int, steps: int, warmup: int, barrier) -> dict:
+    """config_point on every rank (each on its own GPU, same per-GPU shard), reduced like the
+    main line: max over ranks of the wall and kernel times; `value` is the aggregate over
+    all ranks (world x per-GPU bytes / the slowest rank's time)."""
+    from rusty_enet_amd.shards import max_over_ranks
+
+    r = config_point(name, dev, rank, n, steps, warmup, barrier)
+    ms, kms = max_over_ranks([r["ms_per_step"], r["kernel_ms"]])
+    out = dict(r)
+    out.update({"n_gpus": world, "ms_per_step": round(ms, 5), "kernel_ms": round(kms, 5),
+                "value": round(world * r["bytes"] / (ms / 1000.0) / 2**30, 2),
+                "frac": round(r["bytes"] / (kms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4),
+                "note": "value: all ranks' bytes / the slowest rank's time; frac: per GPU, slowest rank"})
+    return out
+
+
 def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, barrier,
                  length: int | None = None) -> dict:
     """One more workload timed on this GPU after the main line (verified on a sample first):
@@ -592,6 +630,14 @@ def main(argv=None) -> int:
     wall_max, kernel_ms_max = max_over_ranks([wall, kernel_ms])
     ms_per_step = wall_max * 1000.0 / args.steps
     extra = {}
+    devices = gather_objects(device_record(dev, rank), world)
+    if world > 1 and args.config == "uniform" and not args.packets_per_gpu:
+        # BASELINE configs[4] (256K x 64 KiB over 8 GPUs): its per-GPU shard on every rank,
+        # in the same process group, after the configs[3] main line.
+        del step, out, spec
+        torch.cuda.empty_cache()
+        extra["large_64k"] = all_ranks_point("large", dev, rank, world, CONFIGS["large"][2], min(args.steps, 50),
+                                             args.warmup, barrier)
     if world == 1 and args.config == "uniform" and not args.no_shard and not args.packets_per_gpu:
         del step, out, spec
         torch.cuda.empty_cache()
@@ -629,6 +675,7 @@ def main(argv=None) -> int:
                          "kernel_ms": round(kernel_ms, 5), "kernel_ms_max_rank": round(kernel_ms_max, 5)},
         }
         line.update(extra)
+        line["devices"] = devices
         if is_range:
             line["data"] = "synthetic compressible ENet-like bytes (tests/_data.enet_like_bytes, seeded)"
             line["config"]["workers"] = RANGE_WORKERS

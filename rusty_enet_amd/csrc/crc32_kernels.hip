@@ -699,7 +699,7 @@ struct UniformBatch {
 typedef __attribute__((address_space(3))) void LdsVoid;
 typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
-constexpr int kRaggedRing = 4;                               // ragged kernel (its round records need LDS too)
+constexpr int kRaggedRing = 3;                               // ragged kernels (3 vs 4: same time)
 constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
 
 // All LDS of a DMA kernel in ONE variable, tables first: the fused asm lookups use
@@ -1283,6 +1283,44 @@ __device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint
       : "memory");
 }
 
+// Per-lane round state from the group's packet record (ragged_record's fields; an invalid
+// group -- past the batch, or a re-read record -- is an empty packet at base4).  Every
+// quantity is derived with 32-bit arithmetic from the precomputed geometry.
+__device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t id,
+                                                         const LaneConsts& c) {
+  const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
+  const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
+  const uint32_t pad = (info >> kRecPadShift) << 2;  // 128 nsteps - 4 nwords
+  const uint32_t v = valid ? (uint32_t)(ax >> kRecVShift) & 3u : 0u;
+  const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
+  RaggedRound rr;
+  rr.ns = max(kRaggedRing, wave_max_over_groups(nsteps));
+  rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
+  rr.top_slot = rr.ns - nsteps;
+  // This lane's chunk at the top step, relative to top: chunk_offset(g, k, nsteps-1, top)
+  // = 4 nwords - 16 (k + 8 (nsteps - 1) + 1) = 112 - 16 k - pad.
+  const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
+  const bool inside = nsteps > 0 && rel > -16;  // not wholly before the packet
+  bool fb = false;                              // chunk_kind == kChunkFallback
+  if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
+    const uint64_t top = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
+    fb = top - c.base4 < (uint64_t)(-rel);
+  }
+  rr.direct = inside && !fb;
+  const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
+  rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
+            (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u);
+  rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+  rr.id = id;
+  // Fast: every packet starts at the same slot (same step count), no fallback chunk,
+  // and the lanes whose top chunk lies before their packet are exactly the ones the
+  // round reads as zeros (ragged_src with !direct).
+  rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
+  rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform || (rr.meta & kMetaFallback)) &&
+            rr.ns <= kRaggedFastMax;
+  return rr;
+}
+
 // Source of this lane's slot-s DMA in round rr (the zero chunk before its top).
 __device__ __forceinline__ uint64_t ragged_src(const RaggedRound& rr, int32_t s, uint64_t dummy) {
   const bool real = s > rr.top_slot || (s == rr.top_slot && rr.direct);
@@ -1341,19 +1379,21 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
   }
 }
 
+// Rounds of packets no longer than the ring (ns == kRaggedRing): top slot T = 0..ring-1.
+template <int... T>
+__device__ __forceinline__ bool ragged_round_short(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
+                                                   const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                                   uint32_t& h3, std::integer_sequence<int, T...>) {
+  return ((cur.top_uniform == T ? (ragged_round_fast<kRaggedRing, T>(cur, nxt, R, c, h0, h1, h2, h3), true) : false) ||
+          ...);
+}
+
 template <int... I>
 __device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRound& cur, const RaggedRound& nxt,
                                                       RaggedRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                       uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
-  if (ns == kRaggedRing) {
-    switch (cur.top_uniform) {
-      case 0: ragged_round_fast<kRaggedRing, 0>(cur, nxt, R, c, h0, h1, h2, h3); return true;
-      case 1: ragged_round_fast<kRaggedRing, 1>(cur, nxt, R, c, h0, h1, h2, h3); return true;
-      case 2: ragged_round_fast<kRaggedRing, 2>(cur, nxt, R, c, h0, h1, h2, h3); return true;
-      case 3: ragged_round_fast<kRaggedRing, 3>(cur, nxt, R, c, h0, h1, h2, h3); return true;
-      default: return false;
-    }
-  }
+  if (ns == kRaggedRing) return ragged_round_short(cur, nxt, R, c, h0, h1, h2, h3,
+                                                   std::make_integer_sequence<int, kRaggedRing>{});
   return ((ns == I + kRaggedRing + 1 ? (ragged_round_fast<I + kRaggedRing + 1>(cur, nxt, R, c, h0, h1, h2, h3), true)
                                      : false) || ...);
 }
@@ -1425,40 +1465,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
     uint64_t ax;
     uint32_t info, id;
     read_record((uint32_t)(uintptr_t)(LdsVoid*)&recb[buf][wv][0], c.grp, ax, info, id);
-    // Everything per lane from the record's precomputed geometry (ragged_record); an
-    // invalid group (past the batch, or a re-read record) is an empty packet at base4.
-    const bool valid = rnd < total_rounds && ((ax >> kRecValidBit) & 1u);
-    const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
-    const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
-    const uint32_t pad = (info >> kRecPadShift) << 2;  // 128 nsteps - 4 nwords
-    const uint32_t v = valid ? (uint32_t)(ax >> kRecVShift) & 3u : 0u;
-    const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
-    RaggedRound rr;
-    rr.ns = max(kDmaRing, wave_max_over_groups(nsteps));
-    rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
-    rr.top_slot = rr.ns - nsteps;
-    // This lane's chunk at the top step, relative to top: chunk_offset(g, k, nsteps-1, top)
-    // = 4 nwords - 16 (k + 8 (nsteps - 1) + 1) = 112 - 16 k - pad.
-    const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
-    const bool inside = nsteps > 0 && rel > -16;  // not wholly before the packet
-    bool fb = false;                              // chunk_kind == kChunkFallback
-    if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
-      const uint64_t top = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
-      fb = top - c.base4 < (uint64_t)(-rel);
-    }
-    rr.direct = inside && !fb;
-    const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
-    rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
-              (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u);
-    rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
-    rr.id = id;
-    // Fast: every packet starts at the same slot (same step count), no fallback chunk,
-    // and the lanes whose top chunk lies before their packet are exactly the ones the
-    // round reads as zeros (ragged_src with !direct).
-    rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
-    rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform || (rr.meta & kMetaFallback)) &&
-              rr.ns <= kRaggedFastMax;
-    return rr;
+    return round_from_record(ax, info, rnd < total_rounds && ((ax >> kRecValidBit) & 1u), id, c);
   };
 
   uint64_t rnd[kLook + 1];
@@ -1518,6 +1525,302 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
   __builtin_amdgcn_s_waitcnt(0);
 }
 
+
+// ---------------------------------------------------------------------------------
+// Ragged kernel with in-kernel job sort (the default ragged path; no pre-pass, no
+// record scratch in HBM).  The batch is cut into jobs of kJobPackets consecutive
+// packets; workgroup b takes jobs b, b + grid, b + 2 grid, ...  One wave builds a job
+// into an LDS job slot: its descriptors arrive by LDS-DMA (phase A), and a round later
+// the wave sorts the job's packets by step class (a counting sort over the 64 lanes,
+// 4 packets per lane, DPP scans) and writes the job's round records into the slot
+// (phase B).  All 16 waves then take the job's rounds from the workgroup's LDS round
+// counter, exactly like the other DMA kernels (dynamic dispatch inside the workgroup),
+// and leave each round's 8 checksums in the slot's result array; the wave that finishes
+// a job's last round writes the job's checksums to HBM with one contiguous 16-B store per
+// lane.  Jobs are built kJobAhead jobs ahead of the rounds being claimed; kJobSlots slots
+// rotate.
+//   * neighbouring packets (which share a 128-B line) are read by one CU within a few
+//     rounds, so the shared line comes from L2 rather than twice from HBM;
+//   * results leave as whole lines (the class-sorted order never reaches HBM);
+//   * the records live in LDS only (the region pre-pass wrote and re-read 16 B per packet
+//     in HBM and cost one more launch).
+// Every LDS access after the first DMA is an asm statement with its own wait (hipcc would
+// order a plain LDS access behind the in-flight LDS-DMAs).  Same round bodies as
+// crc32_ragged_dma_kernel (ragged_round_fast / ragged_round_generic).
+// ---------------------------------------------------------------------------------
+constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
+constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
+constexpr int kJobSlots = 8;                                     // job slots in LDS
+constexpr int kJobAhead = 2;                                     // jobs built ahead of the one claimed
+constexpr uint32_t kJobRoundBytes = 96;                          // per round: u64 ax[8], u32 info[8]
+constexpr uint32_t kJobRecBytes = kJobRounds * kJobRoundBytes;   // 3 KiB, also the descriptor staging
+constexpr int kJobLidShift = 54;                                 // local id (0..255) in ax bits 54..61
+constexpr uint32_t kJobClassWords = 6;                           // 17 classes (16 = no packet), 3 x 10 bits
+constexpr uint32_t kJobSpinLimit = 1u << 22;                     // give up rather than hang (never hit)
+static_assert(kJobPackets == 4 * 64, "4 packets per lane");
+static_assert(kJobRecBytes == kJobPackets * 12, "staging: u64 offsets + u32 lengths");
+
+struct JobSlot {
+  u32x4 rec[kJobRecBytes / 16];
+  uint32_t res[kJobPackets];
+};
+struct RaggedJobsLds {
+  uint32_t tables[kLdsDwords];
+  u32x4 ring[kRaggedRing][kWavesPerBlock][64];
+  JobSlot job[kJobSlots];
+  uint32_t ready[kJobSlots];  // k + 1 once the workgroup's k-th job has its records here
+  uint32_t done[kJobSlots];   // rounds of the job whose checksums are in res
+  uint32_t freed[kJobSlots];  // k + 1 once the k-th job's checksums are in HBM
+  uint32_t next_dispatch;
+};
+static_assert(sizeof(RaggedJobsLds) <= 160 * 1024, "LDS");
+
+struct RaggedJobsBatch {
+  uint64_t base;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
+  uint64_t count;
+  uint64_t njobs;
+};
+
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t a) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint64_t lds_ld64(uint32_t a) {
+  uint64_t v;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ u32x4 lds_ld128(uint32_t a) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st64(uint32_t a, uint64_t v) {
+  asm volatile("ds_write_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
+  uint32_t old;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(old) : "v"(a), "v"(v) : "memory");
+  return old;
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(LdsVoid*)p; }
+
+// Spin (asleep) until the LDS word at `a` equals `want`; false after kJobSpinLimit polls.
+__device__ __forceinline__ bool lds_wait_eq(uint32_t a, uint32_t want) {
+  for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
+    if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
+  constexpr int kDmaRing = kRaggedRing;
+  __shared__ __attribute__((aligned(16))) RaggedJobsLds S;
+  uint32_t* const lds = S.tables;
+  constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
+  if (threadIdx.x < (unsigned)kJobSlots) {
+    S.ready[threadIdx.x] = 0;
+    S.done[threadIdx.x] = 0;
+    S.freed[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kLook;
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(b.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
+
+  auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
+  auto job_count = [&](uint64_t J) -> uint32_t {  // packets in job J (J < njobs)
+    const uint64_t left = b.count - J * kJobPackets;
+    return left < (uint64_t)kJobPackets ? (uint32_t)left : (uint32_t)kJobPackets;
+  };
+  // Round d of this workgroup: round d % 32 of its (d / 32)-th job.  Monotone: once a
+  // round is past the batch, so is every later one.
+  auto round_valid = [&](uint32_t d) -> bool {
+    const uint64_t J = job_of(d / kJobRounds);
+    return J < b.njobs && (uint64_t)(d % kJobRounds) * kPacketsPerWave < job_count(J);
+  };
+
+  // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
+  // u32 lengths at +2048): three 16-B DMAs per lane, or 4-B DMAs (clamped to the batch)
+  // for a partial last job.
+  auto job_dma = [&](uint64_t J, uint32_t slot) {
+    LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
+    const uint64_t p0 = J * kJobPackets;
+    if (job_count(J) == (uint32_t)kJobPackets) {
+      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 2 * lane), (LdsVoid*)st, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 + 2 * lane), (LdsVoid*)(st + 1024), 16, 0,
+                                       0);
+      __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 4 * lane), (LdsVoid*)(st + 2048), 16, 0, 0);
+    } else {
+      const uint32_t* offw = reinterpret_cast<const uint32_t*>(b.offsets);
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i) {
+        const uint64_t w = 64u * i + lane, e = p0 + w / 2;
+        const void* src = e < b.count ? (const void*)(offw + 2 * e + (w & 1u)) : (const void*)g_zero_chunk;
+        __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 256 * i), 4, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        const uint64_t e = p0 + 64u * i + lane;
+        const void* src = e < b.count ? (const void*)(b.lengths + e) : (const void*)g_zero_chunk;
+        __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 2048 + 256 * i), 4, 0, 0);
+      }
+    }
+  };
+  // Phase B (>= kDmaRing DMAs after phase A): sort the job's packets by step class and
+  // write its round records in place of the descriptors; then mark the slot ready.
+  auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
+    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDmaRing - 1) : "memory");
+    const uint32_t st = lds_addr(&S.job[slot].rec[0]);
+    const u32x4 o01 = lds_ld128(st + 32u * lane), o23 = lds_ld128(st + 32u * lane + 16u);
+    const u32x4 ln = lds_ld128(st + 2048u + 16u * lane);
+    const uint64_t off[4] = {o01.x | (uint64_t)o01.y << 32, o01.z | (uint64_t)o01.w << 32,
+                             o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
+    const uint32_t len[4] = {ln.x, ln.y, ln.z, ln.w};
+    const uint32_t n = job_count(J);
+    uint64_t ax[4];
+    uint32_t info[4], cls[4], rank[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool v = 4u * lane + i < n;
+      const RaggedRecord rec = ragged_record(b.base + off[i], len[i], c.base4);
+      ax[i] = v ? rec.ax | ((uint64_t)(4u * lane + i) << kJobLidShift) : 0ull;
+      info[i] = rec.info;
+      cls[i] = v ? (rec.nsteps < kStepClasses - 1 ? rec.nsteps : kStepClasses - 1) : (uint32_t)kStepClasses;
+      rank[i] = 0;
+#pragma unroll
+      for (int j = 0; j < i; ++j) rank[i] += cls[j] == cls[i] ? 1u : 0u;
+    }
+    // Class counts of this lane as 10-bit fields (class c: word c / 3, field c % 3), their
+    // inclusive scan over the lanes, the job's totals, and each class's first position.
+    uint32_t cnt[kJobClassWords], start[kJobClassWords], base[kJobClassWords];
+#pragma unroll
+    for (uint32_t w = 0; w < kJobClassWords; ++w) {
+      cnt[w] = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cnt[w] += cls[i] / 3u == w ? 1u << (10u * (cls[i] % 3u)) : 0u;
+      start[w] = wave_inclusive_add(cnt[w]);
+      base[w] = 0;
+    }
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t cl = 0; cl <= (uint32_t)kStepClasses; ++cl) {
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)start[cl / 3u], 63);
+      base[cl / 3u] |= run << (10u * (cl % 3u));
+      run += (tot >> (10u * (cl % 3u))) & 1023u;
+    }
+#pragma unroll
+    for (uint32_t w = 0; w < kJobClassWords; ++w) start[w] = start[w] - cnt[w] + base[w];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t sw = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kJobClassWords; ++w) sw = cls[i] / 3u == w ? start[w] : sw;
+      const uint32_t q = ((sw >> (10u * (cls[i] % 3u))) & 1023u) + rank[i];
+      const uint32_t r = st + (q >> 3) * kJobRoundBytes;
+      lds_st64(r + 8u * (q & 7u), ax[i]);
+      lds_st32(r + 64u + 4u * (q & 7u), info[i]);
+    }
+    if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
+  };
+
+  // Prologue: waves 0..kJobAhead build the first kJobAhead + 1 jobs (no ring DMA yet).
+  if (wv <= (uint32_t)kJobAhead && job_of(wv) < b.njobs) {
+    job_dma(job_of(wv), wv);
+    __builtin_amdgcn_s_waitcnt(0);
+    job_build(job_of(wv), wv, wv + 1u);
+  }
+  __syncthreads();
+
+  auto make_round = [&](uint32_t d) -> RaggedRound {
+    uint64_t ax = 0;
+    uint32_t info = 0;
+    const uint32_t k = d / kJobRounds, slot = k % kJobSlots;
+    const bool rv = round_valid(d);
+    if (rv && lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u)) {
+      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d % kJobRounds) * kJobRoundBytes;
+      ax = lds_ld64(r + 8u * c.grp);
+      info = lds_ld32(r + 64u + 4u * c.grp);
+    }
+    return round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
+  };
+
+  uint32_t rnd0 = wv, rnd1 = wv + kWavesPerBlock;
+  if (!round_valid(rnd0)) return;
+  RaggedRound cur = make_round(rnd0);
+  RaggedRound nxt = make_round(rnd1);
+  RaggedRing R;
+  R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
+  R.ring0 = lds_addr(&S.ring[0][wv][0]);
+  R.lane16 = lane * 16u;
+  R.q = 0;
+#pragma unroll
+  for (int f = 0; f < kDmaRing; ++f) R.dma(ragged_src(cur, f, c.dummy));  // cur.ns >= kDmaRing
+  R.nextv = read_landed_slot<kDmaRing - 1>(R.next_addr());
+  while (round_valid(rnd0)) {
+    uint32_t d = 0;
+    if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
+    d = __builtin_amdgcn_readfirstlane(d);
+    // Build duty: the claimer of a job's first round builds the job kJobAhead later
+    // (the prologue built jobs 0..kJobAhead).  Its slot must have been flushed.
+    bool build = false;
+    const uint32_t kb = d / kJobRounds + kJobAhead, bslot = kb % kJobSlots;
+    if (d % kJobRounds == 0 && d >= (uint32_t)kJobRounds && job_of(kb) < b.njobs) {
+      build = kb < (uint32_t)kJobSlots ||
+              lds_wait_eq(lds_addr(&S.freed[bslot]), kb - (uint32_t)kJobSlots + 1u);
+      if (build) job_dma(job_of(kb), bslot);
+    }
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    if (!cur.fast ||
+        !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
+                               std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
+      ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
+    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
+    if (cur.meta & kMetaEmpty) reg = kInitRegister;
+    // The round's checksums into the job's result array; the last round of a job
+    // writes the job's checksums to HBM.
+    const uint32_t k0 = rnd0 / kJobRounds, slot0 = k0 % kJobSlots;
+    if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
+    uint32_t old = 0;
+    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
+    old = __builtin_amdgcn_readfirstlane(old);
+    const uint64_t J0 = job_of(k0);
+    const uint32_t n0 = job_count(J0);
+    if (old + 1u == (n0 + kPacketsPerWave - 1) / kPacketsPerWave) {
+      const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
+      uint32_t* dst = out + J0 * kJobPackets + 4u * lane;
+      if (4u * lane + 4u <= n0) {
+        reinterpret_cast<U32x4A4*>(dst)->v = v;
+      } else {
+        if (4u * lane + 0u < n0) dst[0] = v.x;
+        if (4u * lane + 1u < n0) dst[1] = v.y;
+        if (4u * lane + 2u < n0) dst[2] = v.z;
+      }
+      if (lane == 0) {
+        lds_st32(lds_addr(&S.done[slot0]), 0u);
+        lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
+      }
+    }
+    if (build) job_build(job_of(kb), bslot, kb + 1u);
+    const RaggedRound after = make_round(d);
+    rnd0 = rnd1;
+    rnd1 = d;
+    cur = nxt;
+    nxt = after;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
 
 }  // namespace
 
@@ -1753,6 +2056,17 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
+#ifndef ENET_CRC_REGION_RAGGED
+  {
+    // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.
+    const uint64_t njobs = (count + kJobPackets - 1) / kJobPackets;
+    const int cus = cu_count_for_current_device();
+    const unsigned jblocks = (unsigned)(njobs < (uint64_t)cus ? njobs : (uint64_t)cus);
+    const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs};
+    hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+    return hipGetLastError();
+  }
+#endif
   // Region records + the round DMA kernel with XCD-aligned rounds (grid multiple of 8).
   const bool xcd = blocks % 8 == 0 && (uint64_t)blocks * kWavesPerBlock <= kRegionMax;
   const uint32_t region = xcd ? blocks * kWavesPerBlock : kRegionMax;
