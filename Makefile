@@ -11,17 +11,26 @@ HIP_SRC := rusty_enet_amd/csrc/crc32_kernels.hip rusty_enet_amd/csrc/crc32_mailb
 HIP_DEP := $(HIP_SRC) $(wildcard rusty_enet_amd/csrc/*.hpp) include/enet_crc_amd.h include/enet_range_amd.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -fvisibility=hidden -Wall
 
-all: $(LIB) $(ORACLE) $(ORACLE_RANGE)
+# The same sources with compile-time test hooks (a failing staging chunk, a server that
+# never answers a 4095-byte request, a 200-ms call timeout): loaded only by
+# tests/test_gpu_hooks.py through ENET_CRC_AMD_LIB, never by the product.
+TESTLIB := rusty_enet_amd/lib/variants/libenet_crc_amd_testhooks.so
+
+all: $(LIB) $(TESTLIB) $(ORACLE) $(ORACLE_RANGE)
 
 $(LIB): $(HIP_DEP)
 	mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_SRC)
 
+$(TESTLIB): $(HIP_DEP)
+	mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DENET_CRC_TEST_HOOKS -shared -o $@ $(HIP_SRC)
+
 $(ORACLE): oracle/crc32_oracle.c
 	$(CC) -O2 -fPIC -shared -pthread -Wall -o $@ $<
 
 clean:
-	rm -f $(LIB) $(ORACLE) $(ORACLE_RANGE)
+	rm -f $(LIB) $(TESTLIB) $(ORACLE) $(ORACLE_RANGE)
 
 .PHONY: all clean
 

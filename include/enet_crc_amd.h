@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ENET_CRC_ABI_VERSION 4
+#define ENET_CRC_ABI_VERSION 5
 
 #if defined(__GNUC__)
 #define ENET_CRC_API __attribute__((visibility("default")))
@@ -61,17 +61,38 @@ typedef struct enet_crc_ctx enet_crc_ctx;
 /* Most entries in a context's device list. */
 #define ENET_CRC_MAX_LANES 64
 
-/* Per-call modes of enet_crc32_iov (enet_crc_ctx_set_percall_mode). */
-#define ENET_CRC_PERCALL_COPY 0     /* pinned staging -> H2D copy -> kernel -> D2H copy */
-#define ENET_CRC_PERCALL_ZEROCOPY 1 /* kernel reads mapped pinned memory, writes the result to it */
-/* (default) A server wave stays resident on lane 0's device and polls a request mailbox
+/*
+ * Per-call modes of enet_crc32_iov (enet_crc_ctx_set_percall_mode).
+ *
+ * Where the per-call hook stands.  One datagram per call cannot beat the CPU it
+ * replaces: src/crc32.rs runs a 1392-B datagram in ~2.2 us on one host core, while the
+ * fastest GPU mode below costs ~3.4 us from C, of which the PCIe round
+ * trip alone (host store -> GPU -> host) is ~1.7 us.  Installing enet_crc32_iov as
+ * HostSettings::checksum therefore slows every datagram.  The GPU pays off on batches:
+ * the batched receive verify / send insert below (INTEGRATION.md §3 is the recommended
+ * integration), at ~5 TB/s on the device.
+ */
+#define ENET_CRC_PERCALL_COPY 0     /* pinned staging -> H2D copy -> kernel -> D2H copy (~20 us) */
+/* (default) One single-packet launch that reads the gathered bytes from mapped pinned
+ * memory and writes the result to mapped memory; nothing stays resident (~17-19 us). */
+#define ENET_CRC_PERCALL_ZEROCOPY 1
+/* Opt-in.  A server wave stays resident on lane 0's device and polls a request mailbox
  * (device memory the host writes through the PCIe BAR on large-BAR devices, else pinned
- * host memory; answers in pinned host memory): no kernel launch per call.  It exits 20 ms after the last call
- * (the next call relaunches it) and holds one CU while it runs; the context's batch
- * entry points stop it first.  Datagrams above 4096 B take the zero-copy path. */
+ * host memory; answers in pinned host memory): no kernel launch per call (~3.4 us).
+ * Datagrams above 4096 B take the zero-copy path.  While it runs:
+ *   - it holds one CU: every batch launch on that device (any context, and the
+ *     context-free *_device entry points and rings) sizes its grid to the remaining CUs;
+ *   - a device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize())
+ *     waits for it: it exits 20 ms after the last call, or at once on
+ *     enet_crc_ctx_stop_server(), a mode change, a batch entry of the same context or
+ *     enet_crc_ctx_destroy;
+ *   - a call the server does not answer within 5 s stops it, returns ENET_CRC_E_HIP
+ *     (hipErrorLaunchTimeOut) and switches the context back to ZEROCOPY. */
 #define ENET_CRC_PERCALL_PERSISTENT 2
 
-/* ENET_CRC_ABI_VERSION: 4 added enet_crc32_combine; nothing was removed or changed. */
+/* ENET_CRC_ABI_VERSION: 4 added enet_crc32_combine; 5 added enet_crc_ctx_percall_mode and
+ * enet_crc_ctx_stop_server and made ZEROCOPY the default per-call mode.  Nothing was
+ * removed. */
 ENET_CRC_API int enet_crc_abi_version(void);
 ENET_CRC_API const char* enet_crc_strerror(int status);
 /* hipError_t of the last failing HIP call made by this thread (0 if none). */
@@ -97,8 +118,13 @@ ENET_CRC_API int enet_crc_ctx_create_multi(const int* devices, uint32_t ndevices
 ENET_CRC_API void enet_crc_ctx_destroy(enet_crc_ctx* ctx);
 /* Number of lanes (device-list entries) of a context, or ENET_CRC_E_INVALID. */
 ENET_CRC_API int enet_crc_ctx_lanes(const enet_crc_ctx* ctx);
-/* Select how enet_crc32_iov moves one datagram (ENET_CRC_PERCALL_*). */
+/* Select how enet_crc32_iov moves one datagram (ENET_CRC_PERCALL_*; default ZEROCOPY). */
 ENET_CRC_API int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode);
+/* The context's current per-call mode (ENET_CRC_PERCALL_*), or ENET_CRC_E_INVALID. */
+ENET_CRC_API int enet_crc_ctx_percall_mode(enet_crc_ctx* ctx);
+/* Stop the context's persistent server wave now, if one runs (the next persistent-mode
+ * call relaunches it).  Call before a device-wide synchronisation. */
+ENET_CRC_API int enet_crc_ctx_stop_server(enet_crc_ctx* ctx);
 
 /*
  * Byte-balanced contiguous split of a batch into `nshards` packet ranges:
@@ -116,10 +142,10 @@ ENET_CRC_API int enet_crc_shard_bounds(const uint32_t* lengths, uint64_t count, 
  * Replaces: the closure stored in HostSettings::checksum (src/host.rs:40) and
  * called at src/c/protocol.rs:1499 (one slice) and :2287 (up to 65 slices,
  * BUFFER_MAXIMUM, src/consts.rs:37).  Slices may be empty or NULL-with-len-0.
- * Gathers the slices into pinned staging, checksums on the GPU, writes the
- * reference value to *out_crc.  Synchronous.  Zero-copy mode (the default): the
- * kernel reads the gathered bytes from mapped pinned memory and writes the result
- * to mapped memory, no copy-engine transfers (enet_crc_ctx_set_percall_mode).
+ * Gathers the slices into pinned memory, checksums on the GPU, writes the reference
+ * value to *out_crc.  Synchronous.  How the bytes move: the context's per-call mode
+ * (ENET_CRC_PERCALL_*, default ZEROCOPY).  Slower than the CPU per datagram (see the
+ * modes above); batch instead where the protocol loop allows it.
  */
 ENET_CRC_API int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, uint32_t* out_crc);
 

@@ -67,6 +67,8 @@ _SIGNATURES = {
     "enet_crc_ctx_destroy": (None, [ctypes.c_void_p]),
     "enet_crc_ctx_lanes": (ctypes.c_int, [ctypes.c_void_p]),
     "enet_crc_ctx_set_percall_mode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "enet_crc_ctx_percall_mode": (ctypes.c_int, [ctypes.c_void_p]),
+    "enet_crc_ctx_stop_server": (ctypes.c_int, [ctypes.c_void_p]),
     "enet_crc_shard_bounds": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
     "enet_crc32_shards_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     "enet_crc32_iov": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Iov), ctypes.c_size_t, _u32p]),
@@ -117,7 +119,7 @@ ENET_CRC_PERCALL_COPY = 0
 ENET_CRC_PERCALL_ZEROCOPY = 1
 ENET_CRC_PERCALL_PERSISTENT = 2
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 def lib() -> ctypes.CDLL:

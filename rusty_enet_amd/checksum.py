@@ -84,9 +84,22 @@ class Context:
         return lib().enet_crc_ctx_lanes(self._handle)
 
     def set_percall_mode(self, mode: int) -> None:
-        """``_native.ENET_CRC_PERCALL_COPY``, ``ENET_CRC_PERCALL_ZEROCOPY`` or
-        ``ENET_CRC_PERCALL_PERSISTENT`` (default: a resident server wave; include/enet_crc_amd.h)."""
+        """``_native.ENET_CRC_PERCALL_COPY``, ``ENET_CRC_PERCALL_ZEROCOPY`` (the default: one
+        launch per call, nothing resident) or ``ENET_CRC_PERCALL_PERSISTENT`` (opt-in: a
+        resident server wave; include/enet_crc_amd.h has what it holds while it runs)."""
         check(lib().enet_crc_ctx_set_percall_mode(self._handle, mode), "enet_crc_ctx_set_percall_mode")
+
+    @property
+    def percall_mode(self) -> int:
+        mode = lib().enet_crc_ctx_percall_mode(self._handle)
+        if mode < 0:
+            check(mode, "enet_crc_ctx_percall_mode")
+        return mode
+
+    def stop_server(self) -> None:
+        """Stop the persistent server wave now, if one runs (e.g. before a device-wide
+        synchronisation, which would otherwise wait up to its 20-ms idle exit)."""
+        check(lib().enet_crc_ctx_stop_server(self._handle), "enet_crc_ctx_stop_server")
 
     @property
     def handle(self) -> int:

@@ -61,6 +61,12 @@ int fail_hip(hipError_t e) {
 
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_cu_count[kMaxDevices];
+// Persistent per-call server waves that may be resident, per device, over every context
+// of the process.  Each holds one CU for up to 2 s, and the batch kernels' grids are sized
+// to one workgroup per CU with a static share each (a workgroup that finds its CU taken
+// would start only when another finishes, doubling the launch): the grids are sized to
+// the CUs left over instead (cu_count_for_current_device).
+std::atomic<int> g_live_servers[kMaxDevices];
 
 // Restores the caller's current device on scope exit.
 struct DeviceGuard {
@@ -124,14 +130,18 @@ hipError_t device_slot_ladder(const uint32_t** out) {
   return hipSuccess;
 }
 
+// CUs a batch launch on the current device may count on: all of them minus one per
+// persistent server wave that may be resident there (g_live_servers).
 int cu_count_for_current_device() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
   int n = g_cu_count[dev].load(std::memory_order_relaxed);
-  if (n > 0) return n;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-  g_cu_count[dev].store(n, std::memory_order_relaxed);
-  return n;
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    g_cu_count[dev].store(n, std::memory_order_relaxed);
+  }
+  const int live = g_live_servers[dev].load(std::memory_order_acquire);
+  return n - live > 0 ? n - live : 1;
 }
 
 // Byte-balanced contiguous split (the same cut points as rusty_enet_amd/shards.py
@@ -244,9 +254,18 @@ struct PerCall {
   Mailbox* d_req = nullptr;   // its device address
   bool req_vram = false;      // request mailbox in device memory written through the BAR
   hipStream_t mb_stream = nullptr;
-  bool mb_launched = false;   // a server was launched and may still run
+  int mb_device = 0;          // device of mb_stream (lane 0's)
+  bool mb_launched = false;   // a server was launched and may still run (counted in g_live_servers)
   uint32_t mb_seq = 0;        // last request number posted
 };
+
+// The only writer of PerCall::mb_launched: keeps g_live_servers in step with it.
+void set_server_live(PerCall& c, bool live) {
+  if (live == c.mb_launched) return;
+  c.mb_launched = live;
+  if (c.mb_device >= 0 && c.mb_device < kMaxDevices)
+    g_live_servers[c.mb_device].fetch_add(live ? 1 : -1, std::memory_order_acq_rel);
+}
 
 // A worker thread bound to one lane: runs one job at a time for the calling thread.
 class Worker {
@@ -312,7 +331,7 @@ struct enet_crc_ctx {
   std::mutex lock;
   std::vector<Lane> lanes;
   PerCall call;
-  int percall_mode = ENET_CRC_PERCALL_PERSISTENT;
+  int percall_mode = ENET_CRC_PERCALL_ZEROCOPY;
 };
 
 // One slot of a pinned receive ring (include/enet_crc_amd.h).
@@ -340,18 +359,29 @@ struct enet_crc_ring {
 
 namespace {
 
+// A persistent-mode call gives up on the server after this long (test build: 200 ms).
+#ifdef ENET_CRC_TEST_HOOKS
+constexpr std::chrono::milliseconds kMailboxCallTimeout(200);
+#else
+constexpr std::chrono::milliseconds kMailboxCallTimeout(5000);
+#endif
+
 // Host path chunking: at most this many staged bytes / packets per slot.
 constexpr size_t kStageBytes = 64u << 20;
 constexpr size_t kStagePackets = 1u << 18;
 // Concurrent coders of a host-memory range-coder batch (scratch: workers x 64 KiB).
 constexpr uint64_t kRangeHostWorkers = 16384;
 
-// Fault injection for the error-path tests (tests/test_gpu_multi.py): the k-th chunk
-// (1-based) of every enet_crc32_ragged_host shard fails as if its staging allocation had.
+#ifdef ENET_CRC_TEST_HOOKS
+// Test build only (make testhooks; tests/test_gpu_hooks.py): the k-th chunk (1-based) of
+// every enet_crc32_ragged_host shard fails as if its staging allocation had.
 int injected_stage_fault() {
-  const char* v = getenv("ENET_CRC_INJECT_STAGE_FAULT");
+  const char* v = getenv("ENET_CRC_TEST_STAGE_FAULT");
   return v ? atoi(v) : 0;
 }
+#else
+constexpr int injected_stage_fault() { return 0; }
+#endif
 
 // Waits for whatever the lane's slots still have in flight and forgets it (error exits:
 // no copy-out into the caller's buffers, no buffer reuse under a running copy).
@@ -540,7 +570,22 @@ void stop_mailbox(PerCall& c) {
   __atomic_store_n(&c.req->seq, kMailboxStop, __ATOMIC_RELEASE);
   __builtin_ia32_sfence();
   (void)hipStreamSynchronize(c.mb_stream);
-  c.mb_launched = false;
+  set_server_live(c, false);
+}
+
+// After a request timed out: ask the server to exit and wait for its stream at most
+// `limit`.  Returns whether it drained (if not, the wave stays counted as resident).
+bool stop_mailbox_bounded(PerCall& c, std::chrono::milliseconds limit) {
+  if (!c.mb_launched) return true;
+  __atomic_store_n(&c.req->seq, kMailboxStop, __ATOMIC_RELEASE);
+  __builtin_ia32_sfence();
+  const auto t0 = std::chrono::steady_clock::now();
+  while (hipStreamQuery(c.mb_stream) == hipErrorNotReady) {
+    if (std::chrono::steady_clock::now() - t0 > limit) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  set_server_live(c, false);
+  return true;
 }
 
 }  // namespace
@@ -563,6 +608,19 @@ int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode) {
     stop_mailbox(ctx->call);
   }
   ctx->percall_mode = mode;
+  return ENET_CRC_OK;
+}
+
+int enet_crc_ctx_percall_mode(enet_crc_ctx* ctx) {
+  if (!ctx) return ENET_CRC_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  return ctx->percall_mode;
+}
+
+int enet_crc_ctx_stop_server(enet_crc_ctx* ctx) {
+  if (!ctx) return ENET_CRC_E_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->lock);
+  stop_server_for_batch(ctx);
   return ENET_CRC_OK;
 }
 
@@ -723,14 +781,13 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
       memset(c.mb, 0, sizeof(Mailbox));
       ENET_HIP_TRY(hipHostGetDevicePointer((void**)&c.d_mb, c.mb, 0));
       ENET_HIP_TRY(hipStreamCreateWithFlags(&c.mb_stream, hipStreamNonBlocking));
+      c.mb_device = L.device;
       // Requests: in fine-grained device memory that the host writes through the PCIe BAR
       // when the whole VRAM is host-visible (large BAR), so the server reads each
       // datagram locally instead of across PCIe; otherwise the answer
-      // mailbox doubles as the request mailbox.  ENET_CRC_MAILBOX=host forces the latter.
+      // mailbox doubles as the request mailbox.
       int large_bar = 0;
-      const char* mv = getenv("ENET_CRC_MAILBOX");
-      if (!(mv && strcmp(mv, "host") == 0) &&
-          hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, L.device) == hipSuccess && large_bar &&
+      if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, L.device) == hipSuccess && large_bar &&
           hipExtMallocWithFlags((void**)&c.d_req, sizeof(Mailbox), hipDeviceMallocFinegrained) == hipSuccess) {
         c.req = c.d_req;  // one address for host and device
         c.req_vram = true;
@@ -761,7 +818,7 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
     if (c.req_vram) __builtin_ia32_sfence();
     auto launch = [&]() -> hipError_t {
       const hipError_t e = launch_mailbox(c.d_req, c.d_mb, ladder, c.mb_stream);
-      c.mb_launched = e == hipSuccess;
+      set_server_live(c, e == hipSuccess);
       return e;
     };
     if (!c.mb_launched || hipStreamQuery(c.mb_stream) == hipSuccess) ENET_HIP_TRY(launch());
@@ -773,7 +830,14 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
         // The server may have exited (idle limit) just before this request: relaunch.
         if (hipStreamQuery(c.mb_stream) == hipSuccess && (uint32_t)__atomic_load_n(answer, __ATOMIC_ACQUIRE) != seq)
           ENET_HIP_TRY(launch());
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return fail_hip(hipErrorLaunchTimeOut);
+        if (std::chrono::steady_clock::now() - t0 > kMailboxCallTimeout) {
+          // No answer: stop the server (bounded wait) and leave persistent mode for good
+          // on this context, so later calls do not wait for a wedged wave again; the
+          // caller may select persistent mode once more (enet_crc_ctx_set_percall_mode).
+          (void)stop_mailbox_bounded(c, std::chrono::milliseconds(100));
+          ctx->percall_mode = ENET_CRC_PERCALL_ZEROCOPY;
+          return fail_hip(hipErrorLaunchTimeOut);
+        }
       }
       __builtin_ia32_pause();
     }

@@ -27,7 +27,7 @@ def test_header_declares_expected_api():
     assert {"enet_range_compress_ragged_device", "enet_range_decompress_ragged_device",
             "enet_range_scratch_bytes"} <= set(syms)
     assert {"enet_crc_ctx_create_multi", "enet_crc_ctx_lanes", "enet_crc_shard_bounds", "enet_crc32_shards_device",
-            "enet_crc_ctx_set_percall_mode"} <= set(syms)
+            "enet_crc_ctx_set_percall_mode", "enet_crc_ctx_percall_mode", "enet_crc_ctx_stop_server"} <= set(syms)
     assert {"enet_range_compress_iov", "enet_range_decompress", "enet_range_compress_ragged_host",
             "enet_range_decompress_ragged_host"} <= set(syms)
     assert sorted(_native.exported_symbols()) == syms
@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
     lib = _native.lib()
     for name in _declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.enet_crc_abi_version() == _native.ABI_VERSION == 4
+    assert lib.enet_crc_abi_version() == _native.ABI_VERSION == 5
     assert lib.enet_crc_strerror(0) == b"ok"
     assert lib.enet_crc_strerror(_native.ENET_CRC_E_NO_DEVICE) == b"no usable HIP device"
 
