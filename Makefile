@@ -45,3 +45,18 @@ variant: $(HIP_DEP)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o rusty_enet_amd/lib/variants/libenet_crc_amd_$(NAME).so $(HIP_SRC)
 
 .PHONY: variant
+
+# Host code under AddressSanitizer + UBSan: crc32_host.hpp (shard split,
+# slot correction, merge, staging chunks) and the C oracle, built with g++/gcc and run.
+ASAN_FLAGS := -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=all
+asan: tests/cpp/bin/host_asan
+	ASAN_OPTIONS=detect_leaks=1:abort_on_error=0 UBSAN_OPTIONS=print_stacktrace=1 tests/cpp/bin/host_asan
+
+tests/cpp/bin/host_asan: tests/cpp/host_asan.cpp oracle/crc32_oracle.c oracle/range_coder_oracle.c rusty_enet_amd/csrc/crc32_host.hpp rusty_enet_amd/csrc/crc32_slot.hpp rusty_enet_amd/csrc/crc32_ops.hpp
+	mkdir -p tests/cpp/bin
+	$(CC) $(ASAN_FLAGS) -c -o tests/cpp/bin/crc32_oracle_asan.o oracle/crc32_oracle.c
+	$(CC) $(ASAN_FLAGS) -c -o tests/cpp/bin/range_oracle_asan.o oracle/range_coder_oracle.c
+	g++ -std=c++20 $(ASAN_FLAGS) -fconstexpr-ops-limit=1000000000 -o $@ tests/cpp/host_asan.cpp \
+	  tests/cpp/bin/crc32_oracle_asan.o tests/cpp/bin/range_oracle_asan.o -lpthread
+
+.PHONY: asan

@@ -58,6 +58,8 @@ extern "C" {
     pub fn enet_crc_ctx_destroy(ctx: *mut enet_crc_ctx);
     pub fn enet_crc_ctx_lanes(ctx: *const enet_crc_ctx) -> c_int;
     pub fn enet_crc_ctx_set_percall_mode(ctx: *mut enet_crc_ctx, mode: c_int) -> c_int;
+    pub fn enet_crc_ctx_percall_mode(ctx: *mut enet_crc_ctx) -> c_int;
+    pub fn enet_crc_ctx_stop_server(ctx: *mut enet_crc_ctx) -> c_int;
     pub fn enet_crc_shard_bounds(lengths: *const u32, count: u64, nshards: u32, bounds: *mut u64) -> c_int;
     pub fn enet_crc32_shards_device(shards: *const enet_crc_shard, nshards: usize) -> c_int;
     pub fn enet_crc32_iov(ctx: *mut enet_crc_ctx, bufs: *const enet_crc_iov, nbufs: usize, out_crc: *mut u32) -> c_int;
@@ -169,11 +171,22 @@ impl GpuCrc32 {
         Self::with_devices(&devs)
     }
 
-    /// How `crc32` moves one datagram: `ENET_CRC_PERCALL_ZEROCOPY` (default),
-    /// `ENET_CRC_PERCALL_COPY`, or `ENET_CRC_PERCALL_PERSISTENT` (a server wave stays on
-    /// the GPU while calls keep coming: no kernel launch per call).
+    /// How `crc32` moves one datagram: `ENET_CRC_PERCALL_ZEROCOPY` (default: one launch
+    /// per call, nothing resident), `ENET_CRC_PERCALL_COPY`, or `ENET_CRC_PERCALL_PERSISTENT`
+    /// (opt-in: a server wave stays on the GPU while calls keep coming, holding one CU; a
+    /// device-wide synchronize waits for it until `stop_server` or its 20-ms idle exit).
+    /// None of them beats the CPU per datagram; batch instead.
     pub fn set_percall_mode(&self, mode: i32) -> Result<(), CrcError> {
         let st = unsafe { enet_crc_ctx_set_percall_mode(self.ctx.0, mode) };
+        if st != ENET_CRC_OK {
+            return Err(last_error(st));
+        }
+        Ok(())
+    }
+
+    /// Stop the persistent server wave now, if one runs.
+    pub fn stop_server(&self) -> Result<(), CrcError> {
+        let st = unsafe { enet_crc_ctx_stop_server(self.ctx.0) };
         if st != ENET_CRC_OK {
             return Err(last_error(st));
         }

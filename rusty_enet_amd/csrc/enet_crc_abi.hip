@@ -29,6 +29,7 @@
 
 #include "../../include/enet_crc_amd.h"
 #include "../../include/enet_range_amd.h"
+#include "crc32_host.hpp"
 #include "crc32_kernels.hpp"
 #include "crc32_mailbox.hpp"
 #include "crc32_slot.hpp"
@@ -94,17 +95,6 @@ int stream_device(hipStream_t s) {
 // Operator ladder of the slot correction and the flat ragged kernel's finish pass
 // (crc32_slot.hpp: kSlotLevels forward + kInvLevels inverse levels + the M8^len(init) table): one host copy, one
 // device copy per device (uploaded on first use, never freed: 408 KiB).
-const uint32_t* host_slot_ladder() {
-  static uint32_t* ladder = [] {
-    uint32_t* l = new uint32_t[kLadderDwords];
-    build_slot_ladder(l);
-    build_inverse_ladder(l + kSlotLevels * kSlotLevelDwords);
-    build_init_table(l + kLadderLevels * kSlotLevelDwords);
-    return l;
-  }();
-  return ladder;
-}
-
 std::mutex g_ladder_lock;
 uint32_t* g_device_ladder[kMaxDevices];
 
@@ -144,30 +134,6 @@ int cu_count_for_current_device() {
   return n - live > 0 ? n - live : 1;
 }
 
-// Byte-balanced contiguous split (the same cut points as rusty_enet_amd/shards.py
-// shard_bounds): cut k is one past the first packet whose cumulative byte end reaches
-// floor(total * k / n).  lengths == NULL: an even split of `count` packets.
-void split_bounds(const uint32_t* lengths, uint64_t count, uint32_t n, uint64_t* b) {
-  b[0] = 0;
-  b[n] = count;
-  if (!lengths) {
-    for (uint32_t k = 1; k < n; ++k) b[k] = (uint64_t)((unsigned __int128)count * k / n);
-    return;
-  }
-  unsigned __int128 total = 0;
-  for (uint64_t i = 0; i < count; ++i) total += lengths[i];
-  uint64_t i = 0;
-  unsigned __int128 end = count ? lengths[0] : 0;  // byte end of packet i
-  for (uint32_t k = 1; k < n; ++k) {
-    const unsigned __int128 target = total * k / n;
-    if (target == 0 || count == 0) {
-      b[k] = 0;
-      continue;
-    }
-    while (end < target && i + 1 < count) end += lengths[++i];
-    b[k] = i + 1;
-  }
-}
 
 }  // namespace enet_crc
 
@@ -422,22 +388,10 @@ int ragged_host_shard(Lane& L, const uint8_t* base, const uint64_t* h_offsets, c
   while (p < count) {
     StageSlot& s = L.slot[which];
     ENET_TRY(drain(s));
-    // Chunk [p, q): packets whose byte span [lo, hi) fits the staging size.
-    uint64_t lo = h_offsets[p], hi = h_offsets[p] + h_lengths[p];
-    uint64_t q = p + 1;
-    while (q < count && q - p < kStagePackets) {
-      const uint64_t nlo = std::min<uint64_t>(lo, h_offsets[q]);
-      const uint64_t nhi = std::max<uint64_t>(hi, h_offsets[q] + h_lengths[q]);
-      if (nhi - nlo > kStageBytes) break;
-      lo = nlo;
-      hi = nhi;
-      ++q;
-    }
+    const StageChunk ch = plan_stage_chunk(h_offsets, h_lengths, count, p, kStageBytes, kStagePackets);
     if (++chunk == fault_at) return ENET_CRC_E_NOMEM;
-    // Keep the device copy at the same offset mod 4 as the host bytes, so the
-    // kernel sees the same word grid (not required for correctness).
-    const uint64_t lo_al = lo & ~(uint64_t)3;
-    const size_t span = (size_t)(hi - lo_al);
+    const uint64_t q = ch.end, lo_al = ch.lo_al;
+    const size_t span = (size_t)ch.span;
     const size_t n = (size_t)(q - p);
     ENET_TRY(s.bytes.grow(std::max<size_t>(span, 4096), 16));
     ENET_TRY(s.offsets.grow(n));
@@ -716,47 +670,11 @@ int enet_crc32_insert_ragged_device(void* d_base, const uint64_t* d_offsets, con
 }
 
 uint32_t enet_crc32_slot_adjust(uint32_t crc, uint32_t old_slot, uint32_t new_slot, uint32_t bytes_after_slot) {
-  const uint32_t* l = host_slot_ladder();
-  return crc ^ slot_delta(l, kSlotLevels, l, old_slot ^ new_slot, bytes_after_slot);
+  return slot_adjust_checksum(crc, old_slot, new_slot, bytes_after_slot);
 }
 
-// reg(a || b) = M8^n(reg(a) ^ 0xFFFFFFFF) ^ reg(b) with n = |b| (the initial register's
-// share of reg(b) is M8^n(0xFFFFFFFF)), and reg = ~bswap32(checksum), so
-//   checksum(a || b) = bswap32(M8^n(bswap32(crc_a))) ^ crc_b.
-// M8^n = M8^(n mod 4) M32^(n / 4): byte steps, then the host ladder's M32^(2^k) tables
-// (4 lookups per set bit) while n / 4 < 2^32; beyond that by binary powering of M8 as a
-// 32 x 32 GF(2) matrix (column i = M8(1 << i)).
 uint32_t enet_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
-  if (len_b == 0) return crc_a;
-  if ((len_b >> 2) < (1ull << kSlotLevels)) {
-    const uint32_t* l = host_slot_ladder();
-    uint32_t r = __builtin_bswap32(crc_a);
-    for (uint64_t i = 0; i < (len_b & 3u); ++i) r = (r >> 8) ^ kOpTables.sarwate[r & 0xffu];
-    uint64_t q = len_b >> 2;
-    for (int k = 0; q != 0; ++k, q >>= 1)
-      if (q & 1u) r = ladder_apply(l + (size_t)k * kSlotLevelDwords, r);
-    return __builtin_bswap32(r) ^ crc_b;
-  }
-  auto apply = [](const uint32_t* m, uint32_t x) {
-    uint32_t r = 0;
-    for (int i = 0; x != 0; ++i, x >>= 1)
-      if (x & 1u) r ^= m[i];
-    return r;
-  };
-  uint32_t op[32], sq[32];
-  for (int i = 0; i < 32; ++i) {
-    const uint32_t x = 1u << i;
-    op[i] = (x >> 8) ^ kOpTables.sarwate[x & 0xffu];  // M8, src/crc32.rs:43 with a zero byte
-  }
-  uint32_t v = __builtin_bswap32(crc_a);
-  for (uint64_t n = len_b;;) {
-    if (n & 1u) v = apply(op, v);
-    n >>= 1;
-    if (n == 0) break;
-    for (int i = 0; i < 32; ++i) sq[i] = apply(op, op[i]);
-    for (int i = 0; i < 32; ++i) op[i] = sq[i];
-  }
-  return __builtin_bswap32(v) ^ crc_b;
+  return combine_checksums(crc_a, crc_b, len_b);
 }
 
 int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, uint32_t* out_crc) {
