@@ -29,8 +29,7 @@ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 constexpr int kMainLevel = ilog2(4 * kLanesPerPacket);  // M32^(4G) = M32^32
 constexpr int kTreeLevels = ilog2(kLanesPerPacket);
 constexpr uint32_t kTreeDword = kRepDwords;  // unreplicated tree operators M32^4, M32^8, M32^16
-constexpr uint32_t kInvTopDword = kTreeDword + kTreeLevels * 1024;  // inv_top bytes, 4 per dword
-constexpr uint32_t kLdsDwords = kInvTopDword + 64;
+constexpr uint32_t kLdsDwords = kTreeDword + kTreeLevels * 1024;
 static_assert(kMainLevel < kOpLevels, "operator level");
 static_assert(kRepCopies * 4 == 32, "8 copies x 4 tables cover the 32 banks of a ds_read_b32 lane group");
 
@@ -86,9 +85,6 @@ inline void host_lds_image(uint32_t* lds) {
       }
   for (int set = 0; set < kTreeLevels; ++set)
     for (uint32_t r = 0; r < 1024; ++r) lds[kTreeDword + set * 1024 + r] = T.op[set + 2][r >> 8][r & 255];
-  for (uint32_t t = 0; t < 64; ++t)
-    lds[kInvTopDword + t] = T.inv_top[4 * t] | (T.inv_top[4 * t + 1] << 8) | ((uint32_t)T.inv_top[4 * t + 2] << 16) |
-                            ((uint32_t)T.inv_top[4 * t + 3] << 24);
 }
 
 }  // namespace enet_crc
