@@ -1407,7 +1407,9 @@ struct RaggedRound {
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
   bool direct;          // top chunk read directly (not fallback / not before the packet)
   bool fast;            // wave-uniform: every lane's top is the same slot, no fallback, ns <= kRaggedFastMax
+  bool mixed;           // wave-uniform: not fast, but no fallback and ns <= kRaggedFastMax
   int32_t top_uniform;  // that slot (0 unless ns == kRaggedRing and the packets are shorter)
+  int32_t min_top;      // wave-uniform: the earliest top slot of the round's packets
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
@@ -1436,7 +1438,9 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   const uint32_t v = valid ? (uint32_t)(ax >> kRecVShift) & 3u : 0u;
   const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
   RaggedRound rr;
-  rr.ns = max(kRaggedRing, wave_max_over_groups(nsteps));
+  const int32_t max_steps = wave_max_over_groups(nsteps);
+  rr.ns = max(kRaggedRing, max_steps);
+  rr.min_top = rr.ns - max_steps;
   rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
   rr.top_slot = rr.ns - nsteps;
   // This lane's chunk at the top step, relative to top: chunk_offset(g, k, nsteps-1, top)
@@ -1458,8 +1462,13 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   // and the lanes whose top chunk lies before their packet are exactly the ones the
   // round reads as zeros (ragged_src with !direct).
   rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
-  rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform || (rr.meta & kMetaFallback)) &&
-            rr.ns <= kRaggedFastMax;
+  const bool fallback = __builtin_amdgcn_ballot_w64(rr.meta & kMetaFallback) != 0;
+  rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform) && !fallback && rr.ns <= kRaggedFastMax;
+#ifdef ENET_CRC_NO_MIXED
+  rr.mixed = false;  // A/B variant: mixed rounds take the generic path
+#else
+  rr.mixed = !rr.fast && !fallback && rr.ns <= kRaggedFastMax;
+#endif
   return rr;
 }
 
@@ -1521,6 +1530,45 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
   }
 }
 
+// A round whose packets start at different slots (neighbouring step classes meet in a
+// sorted round) and that needs no fallback: the unrolled body of ragged_round_fast with
+// per-lane DMA sources (the zero chunk before each lane's top) and the top masking
+// applied on the slots where some lane has its top.  Every lane's register is 0 until
+// its top slot and reads zeros before it, so the round's first top slot (min_top) needs
+// no lookups and the slots before it are only consumed.
+template <int NS>
+__device__ __forceinline__ void ragged_round_mixed(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
+                                                   const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                                   uint32_t& h3) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const u32x4 v = R.nextv;
+    const int32_t f = s + kRaggedRing;
+    R.dma(f < NS ? ragged_src(cur, f, c.dummy) : ragged_src(nxt, f - NS, c.dummy));
+    if (s < cur.min_top) {
+      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
+      issue_order_fence();
+      continue;
+    }
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    if (s == NS - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
+    const bool top = s == cur.top_slot;
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
+    }
+    if (s == cur.min_top) {
+      h0 = w0;
+      h1 = w1;
+      h2 = w2;
+      h3 = w3;
+      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
+    } else {
+      horner_step_and_read<kRaggedRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, R.next_addr(), R.nextv);
+    }
+    issue_order_fence();
+  }
+}
+
 // Rounds of packets no longer than the ring (ns == kRaggedRing): top slot T = 0..ring-1.
 template <int... T>
 __device__ __forceinline__ bool ragged_round_short(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
@@ -1534,6 +1582,10 @@ template <int... I>
 __device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRound& cur, const RaggedRound& nxt,
                                                       RaggedRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                       uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
+  if (cur.mixed)
+    return ((ns == I + kRaggedRing ? (ragged_round_mixed<I + kRaggedRing>(cur, nxt, R, c, h0, h1, h2, h3), true)
+                                   : false) || ...) ||
+           (ns == kRaggedFastMax ? (ragged_round_mixed<kRaggedFastMax>(cur, nxt, R, c, h0, h1, h2, h3), true) : false);
   if (ns == kRaggedRing) return ragged_round_short(cur, nxt, R, c, h0, h1, h2, h3,
                                                    std::make_integer_sequence<int, kRaggedRing>{});
   return ((ns == I + kRaggedRing + 1 ? (ragged_round_fast<I + kRaggedRing + 1>(cur, nxt, R, c, h0, h1, h2, h3), true)
@@ -1635,7 +1687,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
     uint32_t d = 0;
     if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    if (!cur.fast ||
+    if (!(cur.fast || cur.mixed) ||
         !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
                                std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
       ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
@@ -1923,7 +1975,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
       if (build) job_dma(job_of(kb), bslot);
     }
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    if (!cur.fast ||
+    if (!(cur.fast || cur.mixed) ||
         !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
                                std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
       ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);

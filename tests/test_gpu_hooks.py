@@ -21,6 +21,14 @@ from rusty_enet_amd import _native
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 HOOKS_LIB = os.path.join(REPO, "rusty_enet_amd", "lib", "variants", "libenet_crc_amd_testhooks.so")
