@@ -60,3 +60,10 @@ tests/cpp/bin/host_asan: tests/cpp/host_asan.cpp oracle/crc32_oracle.c oracle/ra
 	  tests/cpp/bin/crc32_oracle_asan.o tests/cpp/bin/range_oracle_asan.o -lpthread
 
 .PHONY: asan
+
+# Measurement probes (tooling, not product): tools/dma_probe.
+probes: tools/dma_probe
+tools/dma_probe: tools/dma_probe.hip rusty_enet_amd/csrc/crc32_layout.hpp rusty_enet_amd/csrc/crc32_ops.hpp
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++20 -o $@ tools/dma_probe.hip
+
+.PHONY: probes

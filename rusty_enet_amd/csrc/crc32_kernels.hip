@@ -1722,7 +1722,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
 
 // ---------------------------------------------------------------------------------
 // Ragged kernel with in-kernel job sort (the default ragged path; no pre-pass, no
-// record scratch in HBM).  The batch is cut into jobs of kJobPackets consecutive
+// record scratch in HBM).  The batch is cut into jobs of up to kJobPackets consecutive
 // packets; workgroup b takes jobs b, b + grid, b + 2 grid, ...  One wave builds a job
 // into an LDS job slot: its descriptors arrive by LDS-DMA (phase A), and a round later
 // the wave sorts the job's packets by step class (a counting sort over the 64 lanes,
@@ -1775,6 +1775,7 @@ struct RaggedJobsBatch {
   const uint32_t* lengths;
   uint64_t count;
   uint64_t njobs;
+  uint32_t job_packets;  // packets per job (<= kJobPackets), chosen so every workgroup gets the same job count
 };
 
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t a) {
@@ -1833,9 +1834,10 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
 
   auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
+  const uint32_t JP = b.job_packets;
   auto job_count = [&](uint64_t J) -> uint32_t {  // packets in job J (J < njobs)
-    const uint64_t left = b.count - J * kJobPackets;
-    return left < (uint64_t)kJobPackets ? (uint32_t)left : (uint32_t)kJobPackets;
+    const uint64_t left = b.count - J * JP;
+    return left < (uint64_t)JP ? (uint32_t)left : JP;
   };
   // Round d of this workgroup: round d % 32 of its (d / 32)-th job.  Monotone: once a
   // round is past the batch, so is every later one.
@@ -1845,12 +1847,13 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   };
 
   // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
-  // u32 lengths at +2048): three 16-B DMAs per lane, or 4-B DMAs (clamped to the batch)
-  // for a partial last job.
+  // u32 lengths at +2048): three 16-B DMAs per lane (kJobPackets descriptors from the
+  // job's first; those past the job are never used), or, near the batch end, 4-B DMAs
+  // clamped to the batch.
   auto job_dma = [&](uint64_t J, uint32_t slot) {
     LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
-    const uint64_t p0 = J * kJobPackets;
-    if (job_count(J) == (uint32_t)kJobPackets) {
+    const uint64_t p0 = J * JP;
+    if (p0 + kJobPackets <= b.count) {
       __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 2 * lane), (LdsVoid*)st, 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 + 2 * lane), (LdsVoid*)(st + 1024), 16, 0,
                                        0);
@@ -1993,7 +1996,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     const uint32_t n0 = job_count(J0);
     if (old + 1u == (n0 + kPacketsPerWave - 1) / kPacketsPerWave) {
       const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
-      uint32_t* dst = out + J0 * kJobPackets + 4u * lane;
+      uint32_t* dst = out + J0 * JP + 4u * lane;
       if (4u * lane + 4u <= n0) {
         reinterpret_cast<U32x4A4*>(dst)->v = v;
       } else {
@@ -2259,11 +2262,19 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   }
 #ifndef ENET_CRC_REGION_RAGGED
   {
-    // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.
-    const uint64_t njobs = (count + kJobPackets - 1) / kJobPackets;
+    // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.  Jobs of up
+    // to kJobPackets packets, sized so that every workgroup gets the same number of jobs
+    // (2048 full jobs on 255 CUs would give 8 workgroups a 9th job: +12 % time).
     const int cus = cu_count_for_current_device();
+    if (cus <= 0) return hipErrorNoDevice;
+    uint64_t njobs = (count + kJobPackets - 1) / kJobPackets;
     const unsigned jblocks = (unsigned)(njobs < (uint64_t)cus ? njobs : (uint64_t)cus);
-    const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs};
+    const uint64_t per_wg = (njobs + jblocks - 1) / jblocks;
+    uint64_t jp = (count + per_wg * jblocks - 1) / (per_wg * jblocks);
+    jp = (jp + kPacketsPerWave - 1) / kPacketsPerWave * kPacketsPerWave;
+    jp = jp < (uint64_t)kJobPackets ? jp : (uint64_t)kJobPackets;
+    njobs = (count + jp - 1) / jp;
+    const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
     hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
     return hipGetLastError();
   }

@@ -10,13 +10,15 @@ mkdir -p "$OUT"
 cd "$ROOT"
 if [ "$K" != "none" ]; then
   if [ -n "$K" ]; then
-    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "$K" --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
+    timeout -k 10 600 python -u -m pytest tests -m gpu -q -k "$K" --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
   else
-    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
+    timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
   fi
   rc=$?
-  tail -3 "$OUT/pytest.log"
-  [ $rc -eq 0 ] || exit $rc
+  grep -E "^(FAILED|ERROR)" "$OUT/pytest.log" | head -20
+  tail -2 "$OUT/pytest.log"
+  # 1 = some tests failed: still time the builds; anything else (crash, timeout): stop
+  [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi
 for i in $(seq 1 "$REPS"); do
   for c in $CFGS; do

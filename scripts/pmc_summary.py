@@ -12,7 +12,7 @@ for path in paths:
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "?")
-            if "crc32" not in name:
+            if not any(f in name for f in os.environ.get("PMC_FILTER", "crc32").split(",")):
                 continue
             key = (row.get("Dispatch_Id"), row.get("Counter_Name"))
             acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
