@@ -697,7 +697,10 @@ struct UniformBatch {
 typedef __attribute__((address_space(3))) void LdsVoid;
 typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
-constexpr int kRaggedRing = 3;                               // ragged kernels (3 vs 4: same time)
+#ifndef ENET_CRC_RAGGED_RING
+#define ENET_CRC_RAGGED_RING 3  // A/B variants may build 4 (with ENET_CRC_JOB_SLOTS=4 for the LDS)
+#endif
+constexpr int kRaggedRing = ENET_CRC_RAGGED_RING;            // ragged kernels (3 vs 4: same time)
 constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
 
 // All LDS of a DMA kernel in ONE variable, tables first: the fused asm lookups use
@@ -1744,7 +1747,10 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
 // ---------------------------------------------------------------------------------
 constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
 constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
-constexpr int kJobSlots = 8;                                     // job slots in LDS
+#ifndef ENET_CRC_JOB_SLOTS
+#define ENET_CRC_JOB_SLOTS 8
+#endif
+constexpr int kJobSlots = ENET_CRC_JOB_SLOTS;                    // job slots in LDS
 constexpr int kJobAhead = 2;                                     // jobs built ahead of the one claimed
 constexpr uint32_t kJobRoundBytes = 96;                          // per round: u64 ax[8], u32 info[8]
 constexpr uint32_t kJobRecBytes = kJobRounds * kJobRoundBytes;   // 3 KiB, also the descriptor staging
@@ -1839,11 +1845,13 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     const uint64_t left = b.count - J * JP;
     return left < (uint64_t)JP ? (uint32_t)left : JP;
   };
-  // Round d of this workgroup: round d % 32 of its (d / 32)-th job.  Monotone: once a
-  // round is past the batch, so is every later one.
+  // Round d of this workgroup: round d % RJ of its (d / RJ)-th job, RJ = JP / 8 rounds
+  // per job (only the batch's last job has fewer).  Monotone: once a round is past the
+  // batch, so is every later one.
+  const uint32_t RJ = JP / kPacketsPerWave;
   auto round_valid = [&](uint32_t d) -> bool {
-    const uint64_t J = job_of(d / kJobRounds);
-    return J < b.njobs && (uint64_t)(d % kJobRounds) * kPacketsPerWave < job_count(J);
+    const uint64_t J = job_of(d / RJ);
+    return J < b.njobs && (uint64_t)(d % RJ) * kPacketsPerWave < job_count(J);
   };
 
   // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
@@ -1931,8 +1939,11 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
   };
 
-  // Prologue: waves 0..kJobAhead build the first kJobAhead + 1 jobs (no ring DMA yet).
-  if (wv <= (uint32_t)kJobAhead && job_of(wv) < b.njobs) {
+  // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
+  // (rounds 0 .. 2 x 16 - 1) and kJobAhead more; the claims of the loop (rounds >= 32)
+  // build the rest.  RJ >= 16 (launch_ragged), so that is at most 2 + kJobAhead jobs.
+  const uint32_t first_jobs = (kWavesPerBlock * kLook - 1) / RJ + kJobAhead + 1;
+  if (wv < first_jobs && job_of(wv) < b.njobs) {
     job_dma(job_of(wv), wv);
     __builtin_amdgcn_s_waitcnt(0);
     job_build(job_of(wv), wv, wv + 1u);
@@ -1942,10 +1953,10 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   auto make_round = [&](uint32_t d) -> RaggedRound {
     uint64_t ax = 0;
     uint32_t info = 0;
-    const uint32_t k = d / kJobRounds, slot = k % kJobSlots;
+    const uint32_t k = d / RJ, slot = k % kJobSlots;
     const bool rv = round_valid(d);
     if (rv && lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u)) {
-      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d % kJobRounds) * kJobRoundBytes;
+      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d % RJ) * kJobRoundBytes;
       ax = lds_ld64(r + 8u * c.grp);
       info = lds_ld32(r + 64u + 4u * c.grp);
     }
@@ -1971,8 +1982,8 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     // Build duty: the claimer of a job's first round builds the job kJobAhead later
     // (the prologue built jobs 0..kJobAhead).  Its slot must have been flushed.
     bool build = false;
-    const uint32_t kb = d / kJobRounds + kJobAhead, bslot = kb % kJobSlots;
-    if (d % kJobRounds == 0 && d >= (uint32_t)kJobRounds && job_of(kb) < b.njobs) {
+    const uint32_t kb = d / RJ + kJobAhead, bslot = kb % kJobSlots;
+    if (d % RJ == 0 && kb >= first_jobs && job_of(kb) < b.njobs) {
       build = kb < (uint32_t)kJobSlots ||
               lds_wait_eq(lds_addr(&S.freed[bslot]), kb - (uint32_t)kJobSlots + 1u);
       if (build) job_dma(job_of(kb), bslot);
@@ -1987,7 +1998,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
     // The round's checksums into the job's result array; the last round of a job
     // writes the job's checksums to HBM.
-    const uint32_t k0 = rnd0 / kJobRounds, slot0 = k0 % kJobSlots;
+    const uint32_t k0 = rnd0 / RJ, slot0 = k0 % kJobSlots;
     if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
@@ -2273,6 +2284,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     uint64_t jp = (count + per_wg * jblocks - 1) / (per_wg * jblocks);
     jp = (jp + kPacketsPerWave - 1) / kPacketsPerWave * kPacketsPerWave;
     jp = jp < (uint64_t)kJobPackets ? jp : (uint64_t)kJobPackets;
+    jp = jp > (uint64_t)kJobPackets / 2 ? jp : (uint64_t)kJobPackets / 2;  // >= 16 rounds per job (the prologue)
     njobs = (count + jp - 1) / jp;
     const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
     hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
