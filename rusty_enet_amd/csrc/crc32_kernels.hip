@@ -1768,9 +1768,10 @@ struct RaggedJobsLds {
   uint32_t tables[kLdsDwords];
   u32x4 ring[kRaggedRing][kWavesPerBlock][64];
   JobSlot job[kJobSlots];
-  uint32_t ready[kJobSlots];  // k + 1 once the workgroup's k-th job has its records here
-  uint32_t done[kJobSlots];   // rounds of the job whose checksums are in res
-  uint32_t freed[kJobSlots];  // k + 1 once the k-th job's checksums are in HBM
+  uint32_t ready[kJobSlots];     // k + 1 once the workgroup's k-th job has its records here
+  uint32_t consumed[kJobSlots];  // rounds of the slot's job whose records have been read
+  uint32_t done[kJobSlots];      // rounds of the job whose checksums are in res
+  uint32_t freed[kJobSlots];     // k + 1 once the k-th job's checksums are in HBM
   uint32_t next_dispatch;
 };
 static_assert(sizeof(RaggedJobsLds) <= 160 * 1024, "LDS");
@@ -1828,6 +1829,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
   if (threadIdx.x < (unsigned)kJobSlots) {
     S.ready[threadIdx.x] = 0;
+    S.consumed[threadIdx.x] = 0;
     S.done[threadIdx.x] = 0;
     S.freed[threadIdx.x] = 0;
   }
@@ -1959,6 +1961,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d % RJ) * kJobRoundBytes;
       ax = lds_ld64(r + 8u * c.grp);
       info = lds_ld32(r + 64u + 4u * c.grp);
+      if (lane == 0) (void)lds_add_rtn(lds_addr(&S.consumed[slot]), 1u);
     }
     return round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
   };
@@ -1979,14 +1982,19 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     uint32_t d = 0;
     if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
     d = __builtin_amdgcn_readfirstlane(d);
-    // Build duty: the claimer of a job's first round builds the job kJobAhead later
-    // (the prologue built jobs 0..kJobAhead).  Its slot must have been flushed.
+    // Build duty: the claimer of a job's first round builds the job kJobAhead later (the
+    // prologue built the first ones) once every round of the slot's previous job has read
+    // its record.  That wait never closes a cycle: a round's record is read at the end of
+    // the iteration that claimed it, and nothing there waits for a younger job (the
+    // checksum slot below waits only for an older job's flush).
     bool build = false;
     const uint32_t kb = d / RJ + kJobAhead, bslot = kb % kJobSlots;
     if (d % RJ == 0 && kb >= first_jobs && job_of(kb) < b.njobs) {
-      build = kb < (uint32_t)kJobSlots ||
-              lds_wait_eq(lds_addr(&S.freed[bslot]), kb - (uint32_t)kJobSlots + 1u);
-      if (build) job_dma(job_of(kb), bslot);
+      build = kb < (uint32_t)kJobSlots || lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ);
+      if (build) {
+        if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
+        job_dma(job_of(kb), bslot);
+      }
     }
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     if (!(cur.fast || cur.mixed) ||
@@ -1999,6 +2007,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     // The round's checksums into the job's result array; the last round of a job
     // writes the job's checksums to HBM.
     const uint32_t k0 = rnd0 / RJ, slot0 = k0 % kJobSlots;
+    if (k0 >= (uint32_t)kJobSlots) (void)lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u);
     if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);

@@ -24,7 +24,7 @@ for i in $(seq 1 "$REPS"); do
   for c in $CFGS; do
     for lib in "$@"; do
       name=$(basename "$lib" .so)
-      ENET_CRC_AMD_LIB="$ROOT/$lib" timeout -k 10 200 python bench.py --config "$c" --cpu-seconds 0 --no-e2e \
+      ENET_CRC_AMD_LIB="$ROOT/$lib" timeout -k 10 150 python bench.py --config "$c" --cpu-seconds 0 --no-e2e \
         --no-shard --steps 60 > "$OUT/${c}_${name}_$i.json" 2> "$OUT/${c}_${name}_$i.err" || exit $?
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['roofline']['kernel_ms'], d['ms_per_step'], d['roofline']['frac'])" \
         "$OUT/${c}_${name}_$i.json" "$c $name run $i"
