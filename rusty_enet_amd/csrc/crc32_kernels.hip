@@ -1869,18 +1869,17 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
                                        0);
       __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 4 * lane), (LdsVoid*)(st + 2048), 16, 0, 0);
     } else {
+      // Not unrolled: one address live at a time (unrolled, hipcc hoisted all twelve out
+      // of the round loop and spilled them to scratch: 18 MB of scratch writes per G2 launch).
       const uint32_t* offw = reinterpret_cast<const uint32_t*>(b.offsets);
-#pragma unroll
-      for (uint32_t i = 0; i < 8; ++i) {
-        const uint64_t w = 64u * i + lane, e = p0 + w / 2;
-        const void* src = e < b.count ? (const void*)(offw + 2 * e + (w & 1u)) : (const void*)g_zero_chunk;
+#pragma unroll 1
+      for (uint32_t i = 0; i < 12; ++i) {
+        const uint32_t w = 64u * (i & 7u) + lane;
+        const uint64_t e = i < 8 ? p0 + w / 2 : p0 + 64u * (i - 8u) + lane;
+        const void* src = e >= b.count ? (const void*)g_zero_chunk
+                          : i < 8    ? (const void*)(offw + 2 * e + (w & 1u))
+                                     : (const void*)(b.lengths + e);
         __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 256 * i), 4, 0, 0);
-      }
-#pragma unroll
-      for (uint32_t i = 0; i < 4; ++i) {
-        const uint64_t e = p0 + 64u * i + lane;
-        const void* src = e < b.count ? (const void*)(b.lengths + e) : (const void*)g_zero_chunk;
-        __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 2048 + 256 * i), 4, 0, 0);
       }
     }
   };
