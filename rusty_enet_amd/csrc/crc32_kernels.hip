@@ -138,11 +138,12 @@ __device__ __forceinline__ int32_t wave_max_over_groups(int32_t v) {
 // dwords 4 (x % 16) .. + 3 of the row: 4 copies of one table entry) goes to lane x of the
 // store, so consecutive lanes write consecutive 16 B (a lane-per-row order had every lane
 // of a ds_write_b128 in the same bank group).  `main` = the Horner operator's level.
-__device__ __forceinline__ void fill_replicated(uint32_t* lds, int main) {
+// `set0` / `set1`: the operator levels of the block's two sets.
+__device__ __forceinline__ void fill_replicated(uint32_t* lds, int set0, int set1 = 0) {
   for (uint32_t x = threadIdx.x; x < kRepDwords / 4; x += kBlock) {
     const uint32_t i = x / (kRowDwords / 4), d = 4u * (x % (kRowDwords / 4));  // row (byte value), first dword
-    const uint32_t set1 = d >= kSetM1Bytes / 4 ? 1u : 0u, tab = (d % (kSetM1Bytes / 4)) / kRepCopies;
-    const uint32_t v = g_op_tables.op[set1 ? 0 : main][tab][i];
+    const uint32_t second = d >= kSetM1Bytes / 4 ? 1u : 0u, tab = (d % (kSetM1Bytes / 4)) / kRepCopies;
+    const uint32_t v = g_op_tables.op[second ? set1 : set0][tab][i];
     reinterpret_cast<u32x4*>(lds)[x] = u32x4{v, v, v, v};
   }
 }
@@ -265,6 +266,30 @@ __device__ __forceinline__ uint32_t combine_tree(const uint32_t* lds, uint32_t h
   if (k == 4u) t = apply_small(lds + kTreeDword + 2048, y);
   y ^= from_lane_plus<4>(t);
   return y;
+}
+
+// combine_tree for the register-ring kernel's layout (kRegsLdsDwords): the first two tree
+// levels through the replicated tree block (conflict-free), the third unreplicated.
+__device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
+                                                    uint32_t h3, const Lookup& lk) {
+  uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
+  y = apply_rep(lds, y, h2, lk.lp1, lk);
+  y = apply_rep(lds, y, h3, lk.lp1, lk);
+  const uint32_t k = threadIdx.x & (G - 1);
+  uint32_t t = 0;
+  if (k & 1u) t = apply_rep(lds + kTreeRepDword, y, 0u, lk.lp, lk);  // M32^4
+  y ^= from_lane_plus<1>(t);
+  if ((k & 3u) == 2u) t = apply_rep(lds + kTreeRepDword, y, 0u, lk.lp1, lk);  // M32^8
+  y ^= from_lane_plus<2>(t);
+  if (k == 4u) t = apply_small(lds + kTree16Dword, y);  // M32^16
+  y ^= from_lane_plus<4>(t);
+  return y;
+}
+
+__device__ __forceinline__ void fill_lds_regs(uint32_t* lds) {
+  fill_replicated(lds, kMainLevel);
+  fill_replicated(lds + kTreeRepDword, 2, 3);
+  for (int x = threadIdx.x; x < 1024; x += kBlock) lds[kTree16Dword + x] = g_op_tables.op[4][x >> 8][x & 255];
 }
 
 // The packet's register (before trailing bytes), valid on lane k == 0 of the group.
@@ -1110,7 +1135,7 @@ __global__ __launch_bounds__(kBlock) void crc32_wave_dma_kernel(UniformBatch u, 
 // loads, same box, alternating).
 // ---------------------------------------------------------------------------------
 struct UniformRegsLds {
-  uint32_t tables[kLdsDwords];
+  uint32_t tables[kRegsLdsDwords];
   uint32_t next_dispatch;
 };
 
@@ -1119,7 +1144,11 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
+#ifdef ENET_CRC_UNREP_TREE
   fill_lds(lds);
+#else
+  fill_lds_regs(lds);
+#endif
   __syncthreads();
   const LaneConsts c = lane_consts(u.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1207,7 +1236,11 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
     }
     q[NS] = load_chunk(entry_src(pbn, NS));
     issue_order_fence();
+#ifdef ENET_CRC_UNREP_TREE  // A/B variant: the unreplicated tree sets of the DMA kernels
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+#else
+    const uint32_t y = combine_tree_rep(lds, h0, h1, h2, h3, c.lk);
+#endif
     uint32_t reg = finish_word(lds, y, z, c.lk);  // every lane; lane k == 0 holds the register
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
@@ -1812,6 +1845,10 @@ __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
   return old;
 }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(LdsVoid*)p; }
+// No-return add, not waited for (the next asm wait on lgkmcnt covers it).
+__device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
+  asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
 
 // Spin (asleep) until the LDS word at `a` equals `want`; false after kJobSpinLimit polls.
 __device__ __forceinline__ bool lds_wait_eq(uint32_t a, uint32_t want) {
@@ -1951,16 +1988,22 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   }
   __syncthreads();
 
+  // Jobs this wave has seen ready / flushed (a job's flags are polled once per wave).
+  uint32_t seen_ready = 0, seen_freed = 0;
   auto make_round = [&](uint32_t d) -> RaggedRound {
     uint64_t ax = 0;
     uint32_t info = 0;
     const uint32_t k = d / RJ, slot = k % kJobSlots;
-    const bool rv = round_valid(d);
-    if (rv && lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u)) {
+    bool rv = round_valid(d);
+    if (rv && k + 1u > seen_ready) {
+      rv = lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u);
+      if (rv) seen_ready = k + 1u;
+    }
+    if (rv) {
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d % RJ) * kJobRoundBytes;
       ax = lds_ld64(r + 8u * c.grp);
       info = lds_ld32(r + 64u + 4u * c.grp);
-      if (lane == 0) (void)lds_add_rtn(lds_addr(&S.consumed[slot]), 1u);
+      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
     }
     return round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
   };
@@ -2006,7 +2049,10 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     // The round's checksums into the job's result array; the last round of a job
     // writes the job's checksums to HBM.
     const uint32_t k0 = rnd0 / RJ, slot0 = k0 % kJobSlots;
-    if (k0 >= (uint32_t)kJobSlots) (void)lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u);
+    if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
+      if (lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u))
+        seen_freed = k0 + 1u - (uint32_t)kJobSlots;
+    }
     if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);

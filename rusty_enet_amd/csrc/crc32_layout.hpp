@@ -30,6 +30,13 @@ constexpr int kMainLevel = ilog2(4 * kLanesPerPacket);  // M32^(4G) = M32^32
 constexpr int kTreeLevels = ilog2(kLanesPerPacket);
 constexpr uint32_t kTreeDword = kRepDwords;  // unreplicated tree operators M32^4, M32^8, M32^16
 constexpr uint32_t kLdsDwords = kTreeDword + kTreeLevels * 1024;
+// Layout of the register-ring kernel (no DMA ring, so LDS has room): a second replicated
+// block at 64 KiB with the first two tree levels (set 0: M32^4, set 1: M32^8; same row
+// format and per-lane addressing as the main block, so the masked tree lookups are
+// bank-conflict-free too), then M32^16 unreplicated (one lane in 8 looks it up).
+constexpr uint32_t kTreeRepDword = kRepDwords;
+constexpr uint32_t kTree16Dword = 2 * kRepDwords;
+constexpr uint32_t kRegsLdsDwords = kTree16Dword + 1024;
 static_assert(kMainLevel < kOpLevels, "operator level");
 static_assert(kRepCopies * 4 == 32, "8 copies x 4 tables cover the 32 banks of a ds_read_b32 lane group");
 
@@ -85,6 +92,21 @@ inline void host_lds_image(uint32_t* lds) {
       }
   for (int set = 0; set < kTreeLevels; ++set)
     for (uint32_t r = 0; r < 1024; ++r) lds[kTreeDword + set * 1024 + r] = T.op[set + 2][r >> 8][r & 255];
+}
+
+// The register-ring kernel's LDS image (kRegsLdsDwords).
+inline void host_lds_image_regs(uint32_t* lds) {
+  const OpTables& T = kOpTables;
+  for (uint32_t x = 0; x < kRegsLdsDwords; ++x) lds[x] = 0;
+  for (uint32_t tab = 0; tab < 4; ++tab)
+    for (uint32_t i = 0; i < 256; ++i)
+      for (uint32_t c = 0; c < kRepCopies; ++c) {
+        lds[i * kRowDwords + tab * kRepCopies + c] = T.op[kMainLevel][tab][i];
+        lds[i * kRowDwords + kSetM1Bytes / 4 + tab * kRepCopies + c] = T.op[0][tab][i];
+        lds[kTreeRepDword + i * kRowDwords + tab * kRepCopies + c] = T.op[2][tab][i];
+        lds[kTreeRepDword + i * kRowDwords + kSetM1Bytes / 4 + tab * kRepCopies + c] = T.op[3][tab][i];
+      }
+  for (uint32_t r = 0; r < 1024; ++r) lds[kTree16Dword + r] = T.op[4][r >> 8][r & 255];
 }
 
 }  // namespace enet_crc
