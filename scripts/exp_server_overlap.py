@@ -1,0 +1,49 @@
+"""Experiment (test-hooks build): G2-shaped ragged batch time with and without a resident
+persistent server wave and with the grid reduced or not (ENET_CRC_TEST_LIVE).
+    ENET_CRC_AMD_LIB=rusty_enet_amd/lib/variants/libenet_crc_amd_testhooks.so python scripts/exp_server_overlap.py"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+from _data import ENET_SEED, packed_offsets, ragged_lengths  # noqa: E402
+
+import rusty_enet_amd as rea  # noqa: E402
+from rusty_enet_amd import _native  # noqa: E402
+
+dev = torch.device("cuda:0")
+for n in (1 << 19, 1 << 20):
+    lengths = ragged_lengths(ENET_SEED, n)
+    offsets = packed_offsets(lengths)
+    data = torch.randint(0, 256, (int(lengths.sum()),), dtype=torch.uint8, device=dev)
+    off = torch.from_numpy(offsets.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def timed(reps=20):
+        rea.crc32_batch(data, offsets=off, lengths=ln, out=out)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            rea.crc32_batch(data, offsets=off, lengths=ln, out=out)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps * 1000
+
+    res = {}
+    for live in ("-1", "1", "2"):
+        os.environ["ENET_CRC_TEST_LIVE"] = live
+        res[f"no server, grid for {live} live"] = timed()
+    with rea.Context(0) as ctx:
+        ctx.set_percall_mode(_native.ENET_CRC_PERCALL_PERSISTENT)
+        for live in ("-1", "1", "2"):
+            os.environ["ENET_CRC_TEST_LIVE"] = live
+            ctx([b"x"])
+            res[f"server live, grid for {live} live"] = timed()
+    os.environ.pop("ENET_CRC_TEST_LIVE")
+    for k, v in res.items():
+        print(f"n={n} {k:36s} {v:8.1f} us", flush=True)

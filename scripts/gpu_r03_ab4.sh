@@ -10,3 +10,7 @@ bash scripts/gpu_ab_configs.sh r03_ab4 "" "uniform" 3 $P $V/libenet_crc_amd_unre
 bash scripts/gpu_ab_configs.sh r03_ab4r none "ragged frag" 2 $P $V/libenet_crc_amd_region.so || exit $?
 bash scripts/gpu_ragged_counters.sh r03_ab4/cnt_uniform $P uniform || exit $?
 bash scripts/gpu_ragged_counters.sh r03_ab4/cnt_jobs $P ragged || exit $?
+mkdir -p gpurun_out/r03_ab4
+ENET_CRC_AMD_LIB="$ROOT/$V/libenet_crc_amd_testhooks.so" timeout -k 10 150 python scripts/exp_server_overlap.py \
+  > gpurun_out/r03_ab4/server_overlap.txt 2>&1 || exit $?
+cat gpurun_out/r03_ab4/server_overlap.txt
