@@ -1275,7 +1275,14 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 //   kNT: 0 plain DMAs, 1 every DMA non-temporal, 2 non-temporal except entries 0 and NS
 //   (the lines a packet shares with its neighbours).
 // ---------------------------------------------------------------------------------
-template <int NS, int kNT>
+//   kShare (back-to-back packets of a multiple of 16 B from a 16-B aligned base): the line
+//   packets g and g + 1 share is read once, whole, by group g + 1 at its entry e* (0 or
+//   1; its lanes before the packet read the previous packet's bytes instead of the zero
+//   chunk, masked for its own register), kept in 4 VGPRs, and handed to group g's lo
+//   lanes at time NS by ds_bpermute with the lane rotation (k + j_{g+1} - j_g) mod 8;
+//   group g's own entry NS is not read (group 7 still reads its part).  Every line of a
+//   round is then one whole-line read: the shape of tools/dma_probe P9.
+template <int NS, int kNT, bool kShare>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   constexpr int R = kUniformRing;
   constexpr int NE = NS + 1;
@@ -1318,9 +1325,21 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
     if (sl != 0) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * sl);
     return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
   };
+  auto jres = [&](uint64_t pb) -> uint32_t { return ((uint32_t)(pb + lx) & 127u) >> 4; };
+  // Entry (0 or 1) of the group whose packet starts at pb that holds the line it shares
+  // with the previous packet (back-to-back packets, kShare).
+  auto estar = [&](uint64_t pb) -> int32_t {
+    const int32_t df = (int32_t)u.stride - 16 * ((int32_t)jres(pb) - (int32_t)jres(pb - u.stride));
+    return NS - df / (int32_t)kBytesPerStep;
+  };
   auto entry_src = [&](uint64_t rnd, int e) -> uint64_t {
     const uint64_t pb = packet_base(rnd);
     const int32_t sl = e - (int32_t)lo_of(pb);
+    if constexpr (kShare) {
+      const uint64_t p = rnd * kPacketsPerWave + c.grp;
+      if (c.grp != 0 && p < u.count && e == estar(pb)) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * sl);
+      if (c.grp != kPacketsPerWave - 1 && e == NS && p + 1 < u.count) return c.dummy;  // from group grp + 1
+    }
     return sl < 0 || sl >= NS ? c.dummy : slot_src(pb, sl);
   };
   auto dma = [&](uint64_t src, uint32_t q, int e) {
@@ -1349,9 +1368,33 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
     const uint32_t lo = lo_of(pb);
     const bool below = is_below(pb);
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    u32x4 keep = {0u, 0u, 0u, 0u};
+    int32_t es = 0;
+    uint32_t src_lane = 0;
+    bool take = false;
+    if constexpr (kShare) {
+      es = estar(pb);
+      src_lane = 4u * ((c.grp + 1u) * G + ((c.k + jres(pb + u.stride) - jres(pb)) & (G - 1u)));
+      take = c.grp != kPacketsPerWave - 1 && rnd[0] * kPacketsPerWave + c.grp + 1 < u.count && lo;
+    }
 #pragma unroll
     for (int t = 0; t < NE; ++t) {
-      const u32x4 v = nextv;
+      u32x4 v = nextv;
+      if constexpr (kShare) {
+        if (t == 0) keep = v;
+        if (t == 1 && es == 1) keep = v;
+        if (t == 0 && lo) v = u32x4{0u, 0u, 0u, 0u};  // slot -1: the previous packet's bytes
+        if (t == NS) {
+          u32x4 x;
+          asm volatile(
+              "ds_bpermute_b32 %0, %4, %5\n\tds_bpermute_b32 %1, %4, %6\n\t"
+              "ds_bpermute_b32 %2, %4, %7\n\tds_bpermute_b32 %3, %4, %8\n\ts_waitcnt lgkmcnt(0)"
+              : "=&v"(x.x), "=&v"(x.y), "=&v"(x.z), "=&v"(x.w)
+              : "v"(src_lane), "v"(keep.x), "v"(keep.y), "v"(keep.z), "v"(keep.w)
+              : "memory");
+          if (take) v = x;
+        }
+      }
       {
         const int f = t + R;  // refill this entry's ring slot R entries ahead
         dma(entry_src(rnd[f / NE], f % NE), q, f % NE);
@@ -2132,8 +2175,12 @@ template <int NS>
 static hipError_t launch_uniform_regs(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
 #ifdef ENET_CRC_LINES_UNIFORM
   if (NS >= 2) {
-    hipLaunchKernelGGL((crc32_uniform_lines_kernel<NS, ENET_CRC_LINES_UNIFORM>), dim3(blocks), dim3(kBlock), 0, stream,
-                       u, out);
+    if (u.stride == u.length && (u.length & 15u) == 0 && (u.base & 15u) == 0 && u.length >= 256)
+      hipLaunchKernelGGL((crc32_uniform_lines_kernel<NS, ENET_CRC_LINES_UNIFORM, true>), dim3(blocks), dim3(kBlock), 0,
+                         stream, u, out);
+    else
+      hipLaunchKernelGGL((crc32_uniform_lines_kernel<NS, ENET_CRC_LINES_UNIFORM, false>), dim3(blocks), dim3(kBlock), 0,
+                         stream, u, out);
     return hipGetLastError();
   }
 #endif
