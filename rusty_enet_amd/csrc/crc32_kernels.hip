@@ -2374,19 +2374,25 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   }
 #ifndef ENET_CRC_REGION_RAGGED
   {
-    // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.  Jobs of up
-    // to kJobPackets packets, sized so that every workgroup gets the same number of jobs
-    // (2048 full jobs on 255 CUs would give 8 workgroups a 9th job: +12 % time).
+    // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.  Workgroups
+    // take jobs statically, so the launch lasts as long as the busiest workgroup's
+    // ceil(njobs / grid) jobs: the job size (16..32 rounds of 8 packets) is the one that
+    // minimises that makespan in rounds (1M packets on 256 CUs: 32 rounds, 16 jobs each;
+    // on 248 CUs: 23 rounds, 23 jobs each instead of 17 or 16 jobs of 32).
     const int cus = cu_count_for_current_device();
     if (cus <= 0) return hipErrorNoDevice;
-    uint64_t njobs = (count + kJobPackets - 1) / kJobPackets;
+    uint64_t jp = kJobPackets, njobs = 0, best = ~0ull;
+    for (uint64_t rj = kJobRounds; rj >= kJobRounds / 2; --rj) {
+      const uint64_t p = rj * kPacketsPerWave, nj = (count + p - 1) / p;
+      const uint64_t grid = nj < (uint64_t)cus ? nj : (uint64_t)cus;
+      const uint64_t span = (nj + grid - 1) / grid * rj;
+      if (span < best) {
+        best = span;
+        jp = p;
+        njobs = nj;
+      }
+    }
     const unsigned jblocks = (unsigned)(njobs < (uint64_t)cus ? njobs : (uint64_t)cus);
-    const uint64_t per_wg = (njobs + jblocks - 1) / jblocks;
-    uint64_t jp = (count + per_wg * jblocks - 1) / (per_wg * jblocks);
-    jp = (jp + kPacketsPerWave - 1) / kPacketsPerWave * kPacketsPerWave;
-    jp = jp < (uint64_t)kJobPackets ? jp : (uint64_t)kJobPackets;
-    jp = jp > (uint64_t)kJobPackets / 2 ? jp : (uint64_t)kJobPackets / 2;  // >= 16 rounds per job (the prologue)
-    njobs = (count + jp - 1) / jp;
     const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
     hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
     return hipGetLastError();

@@ -134,13 +134,13 @@ int cu_count_for_current_device() {
     g_cu_count[dev].store(n, std::memory_order_relaxed);
   }
   constexpr int kXcds = 8;
-  int live = g_live_servers[dev].load(std::memory_order_acquire);
+  const int live = g_live_servers[dev].load(std::memory_order_acquire);
+  int reserve = kXcds * live;
 #ifdef ENET_CRC_TEST_HOOKS
-  // Test build only: ENET_CRC_TEST_LIVE=n counts n servers whether or not any runs, -1 none.
-  if (const char* v = getenv("ENET_CRC_TEST_LIVE")) live = atoi(v) < 0 ? 0 : atoi(v);
+  // Test build only: ENET_CRC_TEST_RESERVE=n holds back n CUs whether or not a server runs.
+  if (const char* v = getenv("ENET_CRC_TEST_RESERVE")) reserve = atoi(v);
 #endif
-  const int usable = n - kXcds * live;
-  return live == 0 ? n : (usable >= kXcds ? usable : kXcds);
+  return n - reserve >= kXcds ? n - reserve : kXcds;
 }
 
 

@@ -1,5 +1,7 @@
 """Experiment (test-hooks build): G2-shaped ragged batch time with and without a resident
-persistent server wave and with the grid reduced or not (ENET_CRC_TEST_LIVE).
+persistent server wave and with 0, 1 or 8 CUs held back (ENET_CRC_TEST_RESERVE).  Only
+the launch stream is synchronised: a device-wide synchronize would wait for the server
+to exit (its 20-ms idle limit) and time the batch without it.
     ENET_CRC_AMD_LIB=rusty_enet_amd/lib/variants/libenet_crc_amd_testhooks.so python scripts/exp_server_overlap.py"""
 import os
 import sys
@@ -25,7 +27,7 @@ for n in (1 << 19, 1 << 20):
 
     def timed(reps=20):
         rea.crc32_batch(data, offsets=off, lengths=ln, out=out)
-        torch.cuda.synchronize()
+        torch.cuda.current_stream().synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):
@@ -35,15 +37,16 @@ for n in (1 << 19, 1 << 20):
         return e0.elapsed_time(e1) / reps * 1000
 
     res = {}
-    for live in ("-1", "1", "2"):
-        os.environ["ENET_CRC_TEST_LIVE"] = live
-        res[f"no server, grid for {live} live"] = timed()
+    for rsv in ("0", "1", "8"):
+        os.environ["ENET_CRC_TEST_RESERVE"] = rsv
+        res[f"no server, {rsv} CUs held back"] = timed()
     with rea.Context(0) as ctx:
         ctx.set_percall_mode(_native.ENET_CRC_PERCALL_PERSISTENT)
-        for live in ("-1", "1", "2"):
-            os.environ["ENET_CRC_TEST_LIVE"] = live
+        for rsv in ("0", "1", "8"):
+            os.environ["ENET_CRC_TEST_RESERVE"] = rsv
             ctx([b"x"])
-            res[f"server live, grid for {live} live"] = timed()
-    os.environ.pop("ENET_CRC_TEST_LIVE")
+            res[f"server live, {rsv} CUs held back"] = timed()
+            assert ctx([b"y"]) == rea.crc32([b"y"])  # still answering
+    os.environ.pop("ENET_CRC_TEST_RESERVE")
     for k, v in res.items():
         print(f"n={n} {k:36s} {v:8.1f} us", flush=True)

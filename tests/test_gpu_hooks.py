@@ -151,10 +151,12 @@ def test_default_mode_leaves_nothing_resident(dev):
 
 
 def _time_launches(fn, reps=20):
+    # Only the launch stream is synchronised: a device-wide synchronize would wait for the
+    # persistent server to exit (20-ms idle limit) and time the batch without it.
     import torch
 
     fn()
-    torch.cuda.synchronize()
+    torch.cuda.current_stream().synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(reps):
