@@ -1144,11 +1144,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
-#ifdef ENET_CRC_UNREP_TREE
-  fill_lds(lds);
-#else
   fill_lds_regs(lds);
-#endif
   __syncthreads();
   const LaneConsts c = lane_consts(u.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1236,11 +1232,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
     }
     q[NS] = load_chunk(entry_src(pbn, NS));
     issue_order_fence();
-#ifdef ENET_CRC_UNREP_TREE  // A/B variant: the unreplicated tree sets of the DMA kernels
-    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-#else
     const uint32_t y = combine_tree_rep(lds, h0, h1, h2, h3, c.lk);
-#endif
     uint32_t reg = finish_word(lds, y, z, c.lk);  // every lane; lane k == 0 holds the register
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
@@ -1260,202 +1252,6 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 }
 
 
-#ifdef ENET_CRC_LINES_UNIFORM
-// ---------------------------------------------------------------------------------
-// Uniform kernel, LDS-DMA form with line-split entries consumed in time order (A/B
-// variant, make variant NAME=lines DEFS=-DENET_CRC_LINES_UNIFORM=<nt mode>).  The ring
-// holds entries, not slots: entry e of a round is, per group, one 128-B line (the
-// register kernel's line-split entries; lane k's chunk of slot e - lo_k).  Every lane
-// consumes entry t at time t, so every ring read waits for vmcnt(R - 1) like the plain
-// DMA kernel (the per-lane entry offset of the parked round-2 "dmas" kernel made every
-// read wait one entry longer).  A lo lane is one slot behind: its slot -1 (time 0) is
-// the zero chunk, its top slot comes at time 1, its last slot at time NS; a hi lane's
-// time NS entry is the zero chunk and its Horner step there is discarded (4 selects).
-// NS + 1 entries per round, NS lookup steps (times 1..NS).
-//   kNT: 0 plain DMAs, 1 every DMA non-temporal, 2 non-temporal except entries 0 and NS
-//   (the lines a packet shares with its neighbours).
-// ---------------------------------------------------------------------------------
-//   kShare (back-to-back packets of a multiple of 16 B from a 16-B aligned base): the line
-//   packets g and g + 1 share is read once, whole, by group g + 1 at its entry e* (0 or
-//   1; its lanes before the packet read the previous packet's bytes instead of the zero
-//   chunk, masked for its own register), kept in 4 VGPRs, and handed to group g's lo
-//   lanes at time NS by ds_bpermute with the lane rotation (k + j_{g+1} - j_g) mod 8;
-//   group g's own entry NS is not read (group 7 still reads its part).  Every line of a
-//   round is then one whole-line read: the shape of tools/dma_probe P9.
-template <int NS, int kNT, bool kShare>
-__global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
-  constexpr int R = kUniformRing;
-  constexpr int NE = NS + 1;
-  __shared__ __attribute__((aligned(16))) UniformDmaLds<R> S;
-  uint32_t* const lds = S.tables;
-  auto& ring = S.ring;
-  uint32_t& next_dispatch = S.next_dispatch;
-  constexpr int kLook = 1 + (NE - 1 + R) / NE;  // rounds a wave must know ahead
-  if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
-  fill_lds(lds);
-  __syncthreads();
-  const LaneConsts c = lane_consts(u.base);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t total_rounds = (u.count + kPacketsPerWave - 1) / kPacketsPerWave;
-  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
-  auto round_of = [&](uint32_t d) -> uint64_t {
-    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
-  };
-  const uint32_t lx = (u.length + 3u) & ~3u, z = lx - u.length;
-  const PacketGeo g = make_geo(0, lx);
-  const uint32_t last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
-  const int64_t rel0 = (int64_t)g.a1 - 16 * (int64_t)(c.k + 1u) - (int64_t)kBytesPerStep * (NS - 1);
-  uint32_t am[4], xm[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    am[j] = rel0 + 4 * j >= 0 ? 0xFFFFFFFFu : 0u;
-    xm[j] = rel0 + 4 * j == 0 ? kInitRegister : 0u;
-  }
-  const bool none0 = rel0 <= -16;
-  const bool part0 = rel0 < 0 && rel0 > -16;
-  const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;
-  auto packet_base = [&](uint64_t rnd) -> uint64_t {
-    const uint64_t p = rnd * kPacketsPerWave + c.grp;
-    return u.base + (p < u.count ? p : u.count - 1) * u.stride;
-  };
-  auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
-  auto lo_of = [&](uint64_t pb) -> uint32_t { return c.k < (((uint32_t)(pb + lx) & 127u) >> 4) ? 1u : 0u; };
-  auto slot_src = [&](uint64_t pb, int32_t sl) -> uint64_t {
-    if (sl != 0) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * sl);
-    return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
-  };
-  auto jres = [&](uint64_t pb) -> uint32_t { return ((uint32_t)(pb + lx) & 127u) >> 4; };
-  // Entry (0 or 1) of the group whose packet starts at pb that holds the line it shares
-  // with the previous packet (back-to-back packets, kShare).
-  auto estar = [&](uint64_t pb) -> int32_t {
-    const int32_t df = (int32_t)u.stride - 16 * ((int32_t)jres(pb) - (int32_t)jres(pb - u.stride));
-    return NS - df / (int32_t)kBytesPerStep;
-  };
-  auto entry_src = [&](uint64_t rnd, int e) -> uint64_t {
-    const uint64_t pb = packet_base(rnd);
-    const int32_t sl = e - (int32_t)lo_of(pb);
-    if constexpr (kShare) {
-      const uint64_t p = rnd * kPacketsPerWave + c.grp;
-      if (c.grp != 0 && p < u.count && e == estar(pb)) return pb + (uint64_t)(rel0 + (int64_t)kBytesPerStep * sl);
-      if (c.grp != kPacketsPerWave - 1 && e == NS && p + 1 < u.count) return c.dummy;  // from group grp + 1
-    }
-    return sl < 0 || sl >= NS ? c.dummy : slot_src(pb, sl);
-  };
-  auto dma = [&](uint64_t src, uint32_t q, int e) {
-    const bool nt = kNT == 1 || (kNT == 2 && e != 0 && e != NS);
-    if (nt)
-      __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 2);
-    else
-      __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, 0);
-  };
-  uint64_t rnd[kLook + 1];
-#pragma unroll
-  for (int i = 0; i < kLook; ++i) rnd[i] = round_of(wv + (uint32_t)(kWavesPerBlock * i));
-  if (rnd[0] >= total_rounds) return;
-  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
-#pragma unroll
-  for (int f = 0; f < R; ++f) dma(entry_src(rnd[f / NE], f % NE), (uint32_t)f, f % NE);
-  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
-  uint32_t q = 0;
-  u32x4 nextv = read_landed_slot<R - 1>(ring0 + lane * 16u);
-  uint32_t res = 0, j = 0;
-  uint64_t res_round = 0;
-  while (rnd[0] < total_rounds) {
-    uint32_t d = 0;
-    if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
-    const uint64_t pb = packet_base(rnd[0]);
-    const uint32_t lo = lo_of(pb);
-    const bool below = is_below(pb);
-    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    u32x4 keep = {0u, 0u, 0u, 0u};
-    int32_t es = 0;
-    uint32_t src_lane = 0;
-    bool take = false;
-    if constexpr (kShare) {
-      es = estar(pb);
-      src_lane = 4u * ((c.grp + 1u) * G + ((c.k + jres(pb + u.stride) - jres(pb)) & (G - 1u)));
-      take = c.grp != kPacketsPerWave - 1 && rnd[0] * kPacketsPerWave + c.grp + 1 < u.count && lo;
-    }
-#pragma unroll
-    for (int t = 0; t < NE; ++t) {
-      u32x4 v = nextv;
-      if constexpr (kShare) {
-        if (t == 0) keep = v;
-        if (t == 1 && es == 1) keep = v;
-        if (t == 0 && lo) v = u32x4{0u, 0u, 0u, 0u};  // slot -1: the previous packet's bytes
-        if (t == NS) {
-          u32x4 x;
-          asm volatile(
-              "ds_bpermute_b32 %0, %4, %5\n\tds_bpermute_b32 %1, %4, %6\n\t"
-              "ds_bpermute_b32 %2, %4, %7\n\tds_bpermute_b32 %3, %4, %8\n\ts_waitcnt lgkmcnt(0)"
-              : "=&v"(x.x), "=&v"(x.y), "=&v"(x.z), "=&v"(x.w)
-              : "v"(src_lane), "v"(keep.x), "v"(keep.y), "v"(keep.z), "v"(keep.w)
-              : "memory");
-          if (take) v = x;
-        }
-      }
-      {
-        const int f = t + R;  // refill this entry's ring slot R entries ahead
-        dma(entry_src(rnd[f / NE], f % NE), q, f % NE);
-        q = q + 1 == (uint32_t)R ? 0u : q + 1;
-      }
-      const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
-      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-      if (t <= 1) {  // the lane's top slot comes at time lo
-        const bool top = (uint32_t)t == lo;
-        if (__builtin_amdgcn_ballot_w64(top && below)) {
-          if (top && below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
-        }
-        if (top) {
-          w0 = (w0 & am[0]) ^ xm[0];
-          w1 = (w1 & am[1]) ^ xm[1];
-          w2 = (w2 & am[2]) ^ xm[2];
-          w3 = (w3 & am[3]) ^ xm[3];
-        }
-      }
-      if (t >= NS - 1) {  // the lane's last slot comes at time NS - 1 + lo
-        if ((uint32_t)t == (uint32_t)(NS - 1) + lo) w3 &= last_mask;
-      }
-      if (t == 0) {  // h = 0 on every lane: M32^32(0) = 0, no lookups
-        h0 = w0;
-        h1 = w1;
-        h2 = w2;
-        h3 = w3;
-        nextv = read_landed_slot<R - 1>(next_addr);
-      } else if (t < NS) {
-        horner_step_and_read<R - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, nextv);
-      } else {  // time NS: only lo lanes have a slot here
-        const uint32_t k0 = h0, k1 = h1, k2 = h2, k3 = h3;
-        horner_step_and_read<R - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, nextv);
-        h0 = lo ? h0 : k0;
-        h1 = lo ? h1 : k1;
-        h2 = lo ? h2 : k2;
-        h3 = lo ? h3 : k3;
-      }
-      issue_order_fence();
-    }
-    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-    const uint32_t reg = finish_word(lds, y, z, c.lk);
-    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
-    if (c.k == j) {
-      res = crc;
-      res_round = rnd[0];
-    }
-#pragma unroll
-    for (int i = 0; i < kLook - 1; ++i) rnd[i] = rnd[i + 1];
-    rnd[kLook - 1] = round_of(__builtin_amdgcn_readfirstlane(d));
-    if (j == 7u || rnd[0] >= total_rounds) {
-      const uint64_t p = res_round * kPacketsPerWave + c.grp;
-      if (c.k <= j && p < u.count) out[p] = res;
-      j = 0;
-    } else {
-      ++j;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-}
-#endif  // ENET_CRC_LINES_UNIFORM
 
 // ---------------------------------------------------------------------------------
 // Ragged kernel, LDS-DMA form.  Packets come sorted by step class (round records from
@@ -2173,17 +1969,6 @@ static unsigned grid_for(uint64_t count, hipError_t& err) {
 
 template <int NS>
 static hipError_t launch_uniform_regs(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
-#ifdef ENET_CRC_LINES_UNIFORM
-  if (NS >= 2) {
-    if (u.stride == u.length && (u.length & 15u) == 0 && (u.base & 15u) == 0 && u.length >= 256)
-      hipLaunchKernelGGL((crc32_uniform_lines_kernel<NS, ENET_CRC_LINES_UNIFORM, true>), dim3(blocks), dim3(kBlock), 0,
-                         stream, u, out);
-    else
-      hipLaunchKernelGGL((crc32_uniform_lines_kernel<NS, ENET_CRC_LINES_UNIFORM, false>), dim3(blocks), dim3(kBlock), 0,
-                         stream, u, out);
-    return hipGetLastError();
-  }
-#endif
   hipLaunchKernelGGL((crc32_uniform_regs_kernel<NS>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
