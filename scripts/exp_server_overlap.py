@@ -1,7 +1,7 @@
 """Experiment (test-hooks build): G2-shaped ragged batch time with and without a resident
-persistent server wave and with 0, 1 or 8 CUs held back (ENET_CRC_TEST_RESERVE).  Only
-the launch stream is synchronised: a device-wide synchronize would wait for the server
-to exit (its 20-ms idle limit) and time the batch without it.
+persistent server wave and with 0 or 8 CUs held back (ENET_CRC_TEST_RESERVE), cases
+interleaved and repeated.  Only the launch stream is synchronised: a device-wide
+synchronize would wait for the server to exit (its 20-ms idle limit).
     ENET_CRC_AMD_LIB=rusty_enet_amd/lib/variants/libenet_crc_amd_testhooks.so python scripts/exp_server_overlap.py"""
 import os
 import sys
@@ -17,6 +17,8 @@ import rusty_enet_amd as rea  # noqa: E402
 from rusty_enet_amd import _native  # noqa: E402
 
 dev = torch.device("cuda:0")
+ctx = rea.Context(0)
+ctx.set_percall_mode(_native.ENET_CRC_PERCALL_PERSISTENT)
 for n in (1 << 19, 1 << 20):
     lengths = ragged_lengths(ENET_SEED, n)
     offsets = packed_offsets(lengths)
@@ -36,17 +38,18 @@ for n in (1 << 19, 1 << 20):
         e1.synchronize()
         return e0.elapsed_time(e1) / reps * 1000
 
-    res = {}
-    for rsv in ("0", "1", "8"):
-        os.environ["ENET_CRC_TEST_RESERVE"] = rsv
-        res[f"no server, {rsv} CUs held back"] = timed()
-    with rea.Context(0) as ctx:
-        ctx.set_percall_mode(_native.ENET_CRC_PERCALL_PERSISTENT)
-        for rsv in ("0", "1", "8"):
-            os.environ["ENET_CRC_TEST_RESERVE"] = rsv
-            ctx([b"x"])
-            res[f"server live, {rsv} CUs held back"] = timed()
-            assert ctx([b"y"]) == rea.crc32([b"y"])  # still answering
-    os.environ.pop("ENET_CRC_TEST_RESERVE")
-    for k, v in res.items():
-        print(f"n={n} {k:36s} {v:8.1f} us", flush=True)
+    for rep in range(3):
+        for server in (False, True):
+            for rsv in ("0", "1", "8"):
+                os.environ["ENET_CRC_TEST_RESERVE"] = rsv
+                if server:
+                    assert ctx([b"x"]) == rea.crc32([b"x"])  # resident from here
+                else:
+                    ctx.stop_server()
+                t = timed()
+                if server:
+                    assert ctx([b"y"]) == rea.crc32([b"y"])  # still answering
+                print(f"n={n} rep={rep} server={'live' if server else 'none':4s} {rsv} CUs held back {t:8.1f} us",
+                      flush=True)
+os.environ.pop("ENET_CRC_TEST_RESERVE")
+ctx.close()
