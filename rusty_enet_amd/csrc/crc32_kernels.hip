@@ -529,19 +529,15 @@ __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, 
 constexpr int kStepClasses = 16;  // ragged sort key: class = min(nsteps, 15)
 
 
-// Round records for crc32_ragged_dma_kernel: sorted position q = 8 r + g goes to
-// record r, group g.  128 B per round, per group: the packet's geometry precomputed
-// (ragged_record) so the round kernel derives every lane's plan with 32-bit arithmetic,
-// and its id (the output index).
-//   bytes  0-63: u64 x 8  a1 | v << 48 | z << 50 | near << 52 | 1 << 53
-//                 a1 = end of the packet run to the next 4-byte boundary (z = 0..3 bytes
-//                 past the end), v = sa & 3, near = top within 16 B of the caller's base
-//                 (only then can a top chunk need the fallback), bit 53 = a packet is here
-//   bytes 64-95: u32 x 8  nsteps | (pad / 4) << 26, pad = 128 nsteps - 4 nwords
-//   bytes 96-127: u32 x 8 packet id
+// A packet's record (ragged_record; written by the job build of crc32_ragged_jobs_kernel
+// into LDS, 12 B per packet): its geometry precomputed so that the round derives every
+// lane's plan with 32-bit arithmetic.
+//   ax   (u64): a1 | v << 48 | z << 50 | near << 52 | 1 << 53 | local id << 54
+//               a1 = end of the packet run to the next 4-byte boundary (z = 0..3 bytes
+//               past the end), v = sa & 3, near = top within 16 B of the caller's base
+//               (only then can a top chunk need the fallback), bit 53 = a packet is here
+//   info (u32): nsteps | (pad / 4) << 26, pad = 128 nsteps - 4 nwords
 // (GPU virtual addresses are below 2^48.)
-constexpr uint32_t kRecordBytes = 128;
-constexpr uint32_t kRecInfoOff = 64, kRecIdOff = 96;
 constexpr uint64_t kRecAddrMask = (1ull << 48) - 1;
 constexpr int kRecVShift = 48, kRecZShift = 50, kRecNearBit = 52, kRecValidBit = 53;
 constexpr uint32_t kRecStepsMask = (1u << 26) - 1;
@@ -567,20 +563,6 @@ __device__ __forceinline__ RaggedRecord ragged_record(uint64_t sa, uint32_t len,
   return r;
 }
 
-// Region records (the default pre-pass): the batch in regions of R consecutive packets,
-// each sorted by step class on its own, stably (address order within a class), into the
-// region's own range of round records.  One workgroup per region, one launch, no global
-// histogram.  Rounds that straddle a class boundary inside a region (at most 15 per
-// region) run the ragged kernel's generic path.  With R = 16 x the ragged kernel's grid,
-// region k = 8 s + x is exactly the set of rounds the workgroups of XCD x take in sweep s
-// (RaggedDmaBatch::xcd_rounds), so the 128-B line two neighbouring packets share is read
-// by the same L2 within one sweep instead of twice from HBM (the global sort separates
-// such neighbours by up to the whole launch).
-constexpr int kRegionPer = 4;                           // packets per thread (consecutive)
-constexpr int kRegionBlock = 1024;
-constexpr int kRegionWaves = kRegionBlock / 64;
-constexpr uint32_t kRegionMax = kRegionPer * kRegionBlock;  // 4096 packets, 64 KiB of records
-
 // Inclusive prefix sum over the 64 lanes in DPP (no LDS round trips): shifts of 1, 2, 4
 // and 8 inside each 16-lane row, then row 0's and row 1's last lanes broadcast into the
 // rows above (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).
@@ -592,99 +574,6 @@ __device__ __forceinline__ uint32_t wave_inclusive_add(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return x;
-}
-
-__global__ __launch_bounds__(kRegionBlock) void crc32_region_records_kernel(Batch<true> b, uint32_t region,
-                                                                             uint8_t* __restrict__ recs) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kRegionMax / kPacketsPerWave * kRecordBytes];
-  __shared__ uint32_t wtot[kRegionWaves][8], wpre[kRegionWaves + 1][8];
-  const uint64_t lo = (uint64_t)blockIdx.x * region;
-  const uint32_t n = (uint32_t)(b.count - lo < region ? b.count - lo : region);
-  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t first = t * kRegionPer;
-  uint64_t sa[kRegionPer];
-  uint32_t len[kRegionPer];
-#pragma unroll
-  for (int k = 0; k < kRegionPer; ++k) {
-    const bool v = first + k < n;
-    sa[k] = v ? b.offsets[lo + first + k] : 0;
-    len[k] = v ? b.lengths[lo + first + k] : 0;
-  }
-  // Class per packet (kStepClasses for the lanes past the region end), each packet's rank
-  // among this thread's packets of its class, and the thread's class counts as 16-bit
-  // fields (class c: word c/2, half c%2).  Static indices only: a dynamically indexed
-  // register array goes to scratch.
-  uint32_t cls[kRegionPer], rank[kRegionPer], cnt[8];
-  const uint64_t base4 = b.base & ~(uint64_t)3;
-  uint32_t info[kRegionPer];
-#pragma unroll
-  for (int k = 0; k < kRegionPer; ++k) {
-    const RaggedRecord rec = ragged_record(b.base + sa[k], len[k], base4);
-    sa[k] = rec.ax;
-    info[k] = rec.info;
-    cls[k] = first + k < n ? (rec.nsteps < kStepClasses - 1 ? rec.nsteps : kStepClasses - 1) : (uint32_t)kStepClasses;
-    rank[k] = 0;
-#pragma unroll
-    for (int j = 0; j < k; ++j) rank[k] += cls[j] == cls[k] ? 1u : 0u;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < 8; ++i) {
-    cnt[i] = 0;
-#pragma unroll
-    for (int k = 0; k < kRegionPer; ++k) cnt[i] += (cls[k] >> 1) == i ? 1u << (16u * (cls[k] & 1u)) : 0u;
-  }
-  // Exclusive prefix over the threads of the block (fields never carry: sums <= 4096):
-  // inclusive scan per wave, then the 16 wave totals scanned by 128 threads.
-  uint32_t inc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) inc[i] = cnt[i];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) inc[i] = wave_inclusive_add(inc[i]);
-  if (lane == 63) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) wtot[wv][i] = inc[i];
-  }
-  __syncthreads();
-  if (t < (kRegionWaves + 1) * 8) {
-    const uint32_t q = t >> 3, i = t & 7u;
-    uint32_t before = 0;
-    for (uint32_t r = 0; r < q; ++r) before += wtot[r][i];
-    wpre[q][i] = before;  // row kRegionWaves: the block totals
-  }
-  __syncthreads();
-  // Start position of each class in this thread: class base (exclusive scan of the
-  // totals over classes) + waves before + lanes before.
-  uint32_t start[8], base = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t tot = wpre[kRegionWaves][i];
-    const uint32_t lo16 = tot & 0xFFFFu, hi16 = tot >> 16;
-    start[i] = wpre[wv][i] + inc[i] - cnt[i] + (base | ((base + lo16) << 16));
-    base += lo16 + hi16;
-  }
-  // The last round of a ragged region keeps zeros in its unused groups.
-  if ((n & 7u) != 0 && t < kRecordBytes / 4)
-    reinterpret_cast<uint32_t*>(stage)[(n / kPacketsPerWave) * (kRecordBytes / 4) + t] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kRegionPer; ++k) {
-    if (first + k >= n) continue;
-    const uint32_t c = cls[k];
-    uint32_t sw = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) sw = (c >> 1) == i ? start[i] : sw;
-    const uint32_t q = ((sw >> (16u * (c & 1u))) & 0xFFFFu) + rank[k];
-    uint8_t* r = stage + (q / kPacketsPerWave) * kRecordBytes;
-    const uint32_t g = q % kPacketsPerWave;
-    reinterpret_cast<uint64_t*>(r)[g] = sa[k];
-    reinterpret_cast<uint32_t*>(r + kRecInfoOff)[g] = info[k];
-    reinterpret_cast<uint32_t*>(r + kRecIdOff)[g] = (uint32_t)(lo + first + k);
-  }
-  __syncthreads();
-  const uint32_t words = (n + kPacketsPerWave - 1) / kPacketsPerWave * (kRecordBytes / 16);
-  u32x4* dst = reinterpret_cast<u32x4*>(recs + lo / kPacketsPerWave * kRecordBytes);
-  const u32x4* src = reinterpret_cast<const u32x4*>(stage);
-  for (uint32_t i = t; i < words; i += kRegionBlock) dst[i] = src[i];
 }
 
 // Uniform batches: base and stride multiples of 4, so every packet has the same
@@ -736,15 +625,7 @@ struct UniformDmaLds {
   u32x4 ring[R][kWavesPerBlock][64];
   uint32_t next_dispatch;
 };
-template <int R>
-struct RaggedDmaLds {
-  uint32_t tables[kLdsDwords];
-  u32x4 ring[R][kWavesPerBlock][64];
-  uint32_t recb[2][kWavesPerBlock][64];
-  uint32_t next_dispatch;
-};
 static_assert(sizeof(UniformDmaLds<kUniformRing>) <= 160 * 1024, "LDS");
-static_assert(sizeof(RaggedDmaLds<kRaggedRing>) <= 160 * 1024, "LDS");
 
 // Wait until at most N DMAs are outstanding, read the landed slot (16 B per lane),
 // and wait for the read (the slot is refilled right after).
@@ -1251,28 +1132,15 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
   }
 }
 
-
-
 // ---------------------------------------------------------------------------------
-// Ragged kernel, LDS-DMA form.  Packets come sorted by step class (round records from
-// crc32_region_records_kernel), so the 8 packets of a round need (nearly) the same
-// number of slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the
-// packets with fewer steps read the zero chunk in their leading slots.  Same ring,
-// dispatch and waits as crc32_uniform_dma_kernel, with per-round, per-lane geometry
-// (streaming kernel's round_meta/mask_top/fallback logic).  Round records join the
-// vector-memory stream as one more DMA per round (4 B per lane: the 128-B record,
-// lanes 32-63 duplicate it), issued two rounds ahead and read with ds_read at the
-// previous round's end, at least kDmaRing-1 DMAs later.  Trailing bytes as in the
-// uniform DMA kernel: each packet runs to the next 4-byte boundary with the bytes
-// past its end masked, then finish_word.
+// Ragged rounds on the LDS-DMA ring (crc32_ragged_jobs_kernel below).  Packets come
+// sorted by step class, so the 8 packets of a round need (nearly) the same number of
+// slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the packets with
+// fewer steps read the zero chunk in their leading slots.  Same ring and waits as
+// crc32_uniform_dma_kernel, with per-round, per-lane geometry from each packet's record
+// (round_from_record).  Trailing bytes as in the uniform DMA kernel: each packet runs to
+// the next 4-byte boundary with the bytes past its end masked, then finish_word.
 // ---------------------------------------------------------------------------------
-struct RaggedDmaBatch {
-  uint64_t base;        // caller's buffer (fallback bound)
-  const uint8_t* recs;  // round records
-  uint64_t count;
-  uint32_t xcd_rounds;  // grid multiple of 8: sweep s of XCD x = one contiguous record range
-};
-
 struct RaggedRound {
   uint64_t cb;          // this lane's chunk address at slot 0
   int32_t ns;           // slots of the round (wave-uniform)
@@ -1288,19 +1156,6 @@ struct RaggedRound {
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
-
-__device__ __forceinline__ void read_record(uint32_t rec_lds, uint32_t grp, uint64_t& addr, uint32_t& info,
-                                            uint32_t& id) {
-  const uint32_t a = rec_lds + 8u * grp, l = rec_lds + kRecInfoOff + 4u * grp, i = rec_lds + kRecIdOff + 4u * grp;
-  asm volatile(
-      "ds_read_b64 %0, %3\n\t"
-      "ds_read_b32 %1, %4\n\t"
-      "ds_read_b32 %2, %5\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(addr), "=&v"(info), "=&v"(id)
-      : "v"(a), "v"(l), "v"(i)
-      : "memory");
-}
 
 // Per-lane round state from the group's packet record (ragged_record's fields; an invalid
 // group -- past the batch, or a re-read record -- is an empty packet at base4).  Every
@@ -1339,11 +1194,7 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
   const bool fallback = __builtin_amdgcn_ballot_w64(rr.meta & kMetaFallback) != 0;
   rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform) && !fallback && rr.ns <= kRaggedFastMax;
-#ifdef ENET_CRC_NO_MIXED
-  rr.mixed = false;  // A/B variant: mixed rounds take the generic path
-#else
   rr.mixed = !rr.fast && !fallback && rr.ns <= kRaggedFastMax;
-#endif
   return rr;
 }
 
@@ -1353,7 +1204,7 @@ __device__ __forceinline__ uint64_t ragged_src(const RaggedRound& rr, int32_t s,
   return real ? rr.cb + (uint64_t)kBytesPerStep * (uint64_t)s : dummy;
 }
 
-// Shared state of one wave's LDS-DMA ring (crc32_ragged_dma_kernel).
+// Shared state of one wave's LDS-DMA ring (crc32_ragged_jobs_kernel).
 struct RaggedRing {
   LdsVoid* slot0;     // this wave's ring position 0
   uint32_t ring0;     // its LDS byte address
@@ -1494,107 +1345,6 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
   }
 }
 
-__global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch b, uint32_t* __restrict__ out) {
-  constexpr int kDmaRing = kRaggedRing;
-  __shared__ __attribute__((aligned(16))) RaggedDmaLds<kDmaRing> S;
-  uint32_t* const lds = S.tables;
-  auto& ring = S.ring;
-  auto& recb = S.recb;
-  uint32_t& next_dispatch = S.next_dispatch;
-  constexpr int kLook = 3;
-  if (threadIdx.x == 0) next_dispatch = kWavesPerBlock * kLook;
-  fill_lds(lds);
-  __syncthreads();
-  const LaneConsts c = lane_consts(b.base);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-
-  const uint64_t total_rounds = (b.count + kPacketsPerWave - 1) / kPacketsPerWave;
-  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
-  // Round of this workgroup's d-th dispatch; increasing in d, a bijection over the grid.
-  // xcd_rounds: workgroup 8 j + x (dispatched to XCD x) takes, in sweep s, the W rounds at
-  // position (j + s) mod J (J = grid / 8) of the range [s sweep + x sweep/8, + sweep/8),
-  // i.e. of the region of crc32_region_records_kernel for XCD x and sweep s.  A region is
-  // sorted by step count, so a fixed position would give workgroup 0 the shortest packets
-  // of every region; the rotation gives every workgroup every position in turn.
-  const uint32_t xcd_j = blockIdx.x >> 3, xcd_nj = gridDim.x >> 3;
-  const uint64_t xcd_base = (uint64_t)(blockIdx.x & 7u) * (sweep / 8);
-  auto round_of = [&](uint32_t d) -> uint64_t {
-    const uint32_t s = d / kWavesPerBlock;
-    if (b.xcd_rounds)
-      return (uint64_t)s * sweep + xcd_base + (uint64_t)((xcd_j + s) % xcd_nj) * kWavesPerBlock + d % kWavesPerBlock;
-    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)s * sweep;
-  };
-  auto dma_record = [&](uint64_t rnd, uint32_t buf) {
-    const uint64_t r = rnd < total_rounds ? rnd : total_rounds - 1;
-    const uint64_t src = (uint64_t)(uintptr_t)b.recs + r * kRecordBytes + 4u * (lane & 31u);
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&recb[buf][wv][0], 4, 0, 0);
-  };
-  auto make_round = [&](uint64_t rnd, uint32_t buf) -> RaggedRound {
-    uint64_t ax;
-    uint32_t info, id;
-    read_record((uint32_t)(uintptr_t)(LdsVoid*)&recb[buf][wv][0], c.grp, ax, info, id);
-    return round_from_record(ax, info, rnd < total_rounds && ((ax >> kRecValidBit) & 1u), id, c);
-  };
-
-  uint64_t rnd[kLook + 1];
-#pragma unroll
-  for (int i = 0; i < kLook; ++i) rnd[i] = round_of(wv + (uint32_t)(kWavesPerBlock * i));
-  if (rnd[0] >= total_rounds) return;
-  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
-  dma_record(rnd[0], 0);
-  dma_record(rnd[1], 1);
-  __builtin_amdgcn_s_waitcnt(0);  // prologue only: both records landed (no other LDS-DMA yet)
-  RaggedRound cur = make_round(rnd[0], 0);
-  RaggedRound nxt = make_round(rnd[1], 1);
-  dma_record(rnd[2], 0);  // read one round from now
-  RaggedRing R;
-  R.slot0 = (LdsVoid*)&ring[0][wv][0];
-  R.ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
-  R.lane16 = lane * 16u;
-  R.q = 0;
-#pragma unroll
-  for (int f = 0; f < kDmaRing; ++f) R.dma(ragged_src(cur, f, c.dummy));  // cur.ns >= kDmaRing
-  R.nextv = read_landed_slot<kDmaRing - 1>(R.next_addr());
-  uint32_t res = 0, res_id = 0, j = 0;
-  bool res_valid = false;
-  while (rnd[0] < total_rounds) {
-    uint32_t d = 0;
-    if (lane == 0) d = lds_fetch_add_one(&next_dispatch);
-    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    if (!(cur.fast || cur.mixed) ||
-        !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
-                               std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
-      ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
-    // Round end (record rnd[2] has landed: >= kDmaRing-1 DMAs since it was issued).
-    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds the register
-    if (cur.meta & kMetaEmpty) reg = kInitRegister;
-    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
-    if (c.k == j) {
-      res = crc;
-      res_id = cur.id;
-      res_valid = (cur.meta & kMetaStore) != 0;
-    }
-    const RaggedRound after = make_round(rnd[2], 0);
-    rnd[3] = round_of(__builtin_amdgcn_readfirstlane(d));
-    dma_record(rnd[3], 0);  // buffer 0 is free again: rnd[2]'s record was just read
-    rnd[0] = rnd[1];
-    rnd[1] = rnd[2];
-    rnd[2] = rnd[3];
-    cur = nxt;
-    nxt = after;
-    if (j == 7u || rnd[0] >= total_rounds) {
-      if (c.k <= j && res_valid) out[res_id] = res;
-      j = 0;
-    } else {
-      ++j;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-}
-
-
 // ---------------------------------------------------------------------------------
 // Ragged kernel with in-kernel job sort (the default ragged path; no pre-pass, no
 // record scratch in HBM).  The batch is cut into jobs of up to kJobPackets consecutive
@@ -1611,11 +1361,11 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_dma_kernel(RaggedDmaBatch
 //   * neighbouring packets (which share a 128-B line) are read by one CU within a few
 //     rounds, so the shared line comes from L2 rather than twice from HBM;
 //   * results leave as whole lines (the class-sorted order never reaches HBM);
-//   * the records live in LDS only (the region pre-pass wrote and re-read 16 B per packet
+//   * the records live in LDS only (round 2's region pre-pass wrote and re-read 16 B per packet
 //     in HBM and cost one more launch).
 // Every LDS access after the first DMA is an asm statement with its own wait (hipcc would
 // order a plain LDS access behind the in-flight LDS-DMAs).  Same round bodies as
-// crc32_ragged_dma_kernel (ragged_round_fast / ragged_round_generic).
+// round 2's region kernel (ragged_round_fast / _mixed / _generic).
 // ---------------------------------------------------------------------------------
 constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
 constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
@@ -2042,107 +1792,6 @@ hipError_t launch_single(const uint8_t* base, uint32_t length, uint32_t* out, hi
   return L.streaming();
 }
 
-// Stream-ordered scratch for the ragged pre-pass comes from a pool of our own with an
-// unlimited release threshold: freed blocks stay cached, so the per-launch
-// hipMallocFromPoolAsync / hipFreeAsync pair costs no remapping (the default pool,
-// threshold 0, hands memory back at every synchronisation).
-constexpr int kMaxPoolDevices = 64;
-static hipError_t scratch_pool(hipMemPool_t* out) {
-  static std::mutex lock;
-  static hipMemPool_t pools[kMaxPoolDevices];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= kMaxPoolDevices) return hipErrorInvalidDevice;
-  std::lock_guard<std::mutex> g(lock);
-  if (!pools[dev]) {
-    hipMemPoolProps props = {};
-    props.allocType = hipMemAllocationTypePinned;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = dev;
-    hipMemPool_t p = nullptr;
-    e = hipMemPoolCreate(&p, &props);
-    if (e != hipSuccess) return e;
-    uint64_t keep = ~0ull;
-    e = hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
-    if (e != hipSuccess) {
-      (void)hipMemPoolDestroy(p);
-      return e;
-    }
-    pools[dev] = p;
-  }
-  *out = pools[dev];
-  return hipSuccess;
-}
-
-// Round-record scratch of the default ragged path, kept per (device, stream) and reused
-// by the next launch on that stream (stream order makes the reuse safe), grown
-// stream-ordered when a batch needs more.  A hipMallocFromPoolAsync / hipFreeAsync pair
-// per launch left the GPU idle ~6 us between consecutive ragged launches (kernel
-// trace).  Up to kStreamScratchSlots streams are cached; launches on
-// further streams allocate per launch as before.  (A stream handle that is destroyed
-// and handed out again by HIP inherits its predecessor's buffer; a stream's pending
-// work completes before its handle can be reused, so the reuse stays ordered.)
-constexpr int kStreamScratchSlots = 64;
-struct StreamScratch {
-  int dev = -1;
-  hipStream_t stream = nullptr;
-  void* ptr = nullptr;
-  size_t bytes = 0;
-};
-static std::mutex g_stream_scratch_lock;
-static StreamScratch g_stream_scratch[kStreamScratchSlots];
-
-// *owned = false: the buffer stays cached (do not free it after the launch).  Returns
-// with `held` locked: the caller launches the kernels that use the buffer before it
-// unlocks, so another thread on the same stream cannot free or regrow the buffer
-// ahead of those launches in stream order.
-static hipError_t records_scratch(hipStream_t stream, size_t need, hipMemPool_t pool, void** out, bool* owned,
-                                  std::unique_lock<std::mutex>& held) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  const char* v = getenv("ENET_CRC_SCRATCH_CACHE");
-  const bool cache = !(v && strcmp(v, "0") == 0);
-  held = std::unique_lock<std::mutex>(g_stream_scratch_lock);
-  StreamScratch* slot = nullptr;
-  for (StreamScratch& s : g_stream_scratch) {
-    if (s.dev == dev && s.stream == stream) {
-      slot = &s;
-      break;
-    }
-    if (!slot && s.dev < 0) slot = &s;  // first free slot, unless the stream has one further on
-  }
-  if (!cache || !slot) {
-    *owned = true;
-    return hipMallocFromPoolAsync(out, need, pool, stream);
-  }
-  if (slot->dev == dev && slot->stream == stream && slot->bytes >= need) {
-    *owned = false;
-    *out = slot->ptr;
-    return hipSuccess;
-  }
-  if (slot->ptr) {
-    e = hipFreeAsync(slot->ptr, stream);  // same stream: after every earlier use
-    slot->ptr = nullptr;
-    slot->bytes = 0;
-    if (e != hipSuccess) return e;
-  }
-  const size_t grow = need + need / 4;
-  e = hipMallocFromPoolAsync(&slot->ptr, grow, pool, stream);
-  if (e != hipSuccess) {
-    slot->ptr = nullptr;
-    slot->dev = -1;
-    return e;
-  }
-  slot->dev = dev;
-  slot->stream = stream;
-  slot->bytes = grow;
-  *owned = false;
-  *out = slot->ptr;
-  return hipSuccess;
-}
-
 // Below this many packets the sort costs more than the padding it saves.
 constexpr uint64_t kSortMinPackets = 4096;
 
@@ -2157,53 +1806,28 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-#ifndef ENET_CRC_REGION_RAGGED
-  {
-    // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.  Workgroups
-    // take jobs statically, so the launch lasts as long as the busiest workgroup's
-    // ceil(njobs / grid) jobs: the job size (16..32 rounds of 8 packets) is the one that
-    // minimises that makespan in rounds (1M packets on 256 CUs: 32 rounds, 16 jobs each;
-    // on 248 CUs: 23 rounds, 23 jobs each instead of 17 or 16 jobs of 32).
-    const int cus = cu_count_for_current_device();
-    if (cus <= 0) return hipErrorNoDevice;
-    uint64_t jp = kJobPackets, njobs = 0, best = ~0ull;
-    for (uint64_t rj = kJobRounds; rj >= kJobRounds / 2; --rj) {
-      const uint64_t p = rj * kPacketsPerWave, nj = (count + p - 1) / p;
-      const uint64_t grid = nj < (uint64_t)cus ? nj : (uint64_t)cus;
-      const uint64_t span = (nj + grid - 1) / grid * rj;
-      if (span < best) {
-        best = span;
-        jp = p;
-        njobs = nj;
-      }
+  // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.  Workgroups
+  // take jobs statically, so the launch lasts as long as the busiest workgroup's
+  // ceil(njobs / grid) jobs: the job size (16..32 rounds of 8 packets) is the one that
+  // minimises that makespan in rounds (1M packets on 256 CUs: 32 rounds, 16 jobs each;
+  // on 248 CUs: 23 rounds, 23 jobs each instead of 17 or 16 jobs of 32).
+  const int cus = cu_count_for_current_device();
+  if (cus <= 0) return hipErrorNoDevice;
+  uint64_t jp = kJobPackets, njobs = 0, best = ~0ull;
+  for (uint64_t rj = kJobRounds; rj >= kJobRounds / 2; --rj) {
+    const uint64_t p = rj * kPacketsPerWave, nj = (count + p - 1) / p;
+    const uint64_t grid = nj < (uint64_t)cus ? nj : (uint64_t)cus;
+    const uint64_t span = (nj + grid - 1) / grid * rj;
+    if (span < best) {
+      best = span;
+      jp = p;
+      njobs = nj;
     }
-    const unsigned jblocks = (unsigned)(njobs < (uint64_t)cus ? njobs : (uint64_t)cus);
-    const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
-    hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
-    return hipGetLastError();
   }
-#endif
-  // Region records + the round DMA kernel with XCD-aligned rounds (grid multiple of 8).
-  const bool xcd = blocks % 8 == 0 && (uint64_t)blocks * kWavesPerBlock <= kRegionMax;
-  const uint32_t region = xcd ? blocks * kWavesPerBlock : kRegionMax;
-  const uint64_t nregions = (count + region - 1) / region;
-  const uint64_t rounds = (count + kPacketsPerWave - 1) / kPacketsPerWave;
-  void* scratch = nullptr;
-  hipMemPool_t pool = nullptr;
-  err = scratch_pool(&pool);
-  if (err != hipSuccess) return err;
-  bool owned = true;
-  std::unique_lock<std::mutex> held;  // until both launches are enqueued
-  err = records_scratch(stream, (size_t)rounds * kRecordBytes, pool, &scratch, &owned, held);
-  if (err != hipSuccess) return err;
-  uint8_t* recs = static_cast<uint8_t*>(scratch);
-  hipLaunchKernelGGL(crc32_region_records_kernel, dim3((unsigned)nregions), dim3(kRegionBlock), 0, stream, b,
-                     region, recs);
-  const RaggedDmaBatch rb{b.base, recs, count, xcd ? 1u : 0u};
-  hipLaunchKernelGGL(crc32_ragged_dma_kernel, dim3(blocks), dim3(kBlock), 0, stream, rb, out);
-  err = hipGetLastError();
-  const hipError_t ferr = owned ? hipFreeAsync(scratch, stream) : hipSuccess;
-  return err != hipSuccess ? err : ferr;
+  const unsigned jblocks = (unsigned)(njobs < (uint64_t)cus ? njobs : (uint64_t)cus);
+  const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
+  hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+  return hipGetLastError();
 }
 
 }  // namespace enet_crc
