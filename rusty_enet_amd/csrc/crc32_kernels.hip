@@ -1439,10 +1439,25 @@ __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
+#ifdef ENET_CRC_SPIN_STATS
+// Measurement build only (make variant NAME=spin DEFS=-DENET_CRC_SPIN_STATS): failed polls
+// and waits per wait site, read back with enet_crc_debug_spin_stats.
+__device__ unsigned long long g_spin_stats[8];
+#endif
+
 // Spin (asleep) until the LDS word at `a` equals `want`; false after kJobSpinLimit polls.
+template <int kSite = 0>
 __device__ __forceinline__ bool lds_wait_eq(uint32_t a, uint32_t want) {
   for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
-    if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) return true;
+    if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) {
+#ifdef ENET_CRC_SPIN_STATS
+      if ((threadIdx.x & 63u) == 0) {
+        atomicAdd(&g_spin_stats[2 * kSite], (unsigned long long)i);
+        atomicAdd(&g_spin_stats[2 * kSite + 1], i ? 1ull : 0ull);
+      }
+#endif
+      return true;
+    }
     __builtin_amdgcn_s_sleep(2);
   }
   return false;
@@ -1585,7 +1600,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     const uint32_t k = d / RJ, slot = k % kJobSlots;
     bool rv = round_valid(d);
     if (rv && k + 1u > seen_ready) {
-      rv = lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u);
+      rv = lds_wait_eq<0>(lds_addr(&S.ready[slot]), k + 1u);
       if (rv) seen_ready = k + 1u;
     }
     if (rv) {
@@ -1621,7 +1636,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     bool build = false;
     const uint32_t kb = d / RJ + kJobAhead, bslot = kb % kJobSlots;
     if (d % RJ == 0 && kb >= first_jobs && job_of(kb) < b.njobs) {
-      build = kb < (uint32_t)kJobSlots || lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ);
+      build = kb < (uint32_t)kJobSlots || lds_wait_eq<1>(lds_addr(&S.consumed[bslot]), RJ);
       if (build) {
         if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
         job_dma(job_of(kb), bslot);
@@ -1639,7 +1654,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     // writes the job's checksums to HBM.
     const uint32_t k0 = rnd0 / RJ, slot0 = k0 % kJobSlots;
     if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
-      if (lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u))
+      if (lds_wait_eq<2>(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
     }
     if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
@@ -1831,3 +1846,17 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
 }
 
 }  // namespace enet_crc
+
+#ifdef ENET_CRC_SPIN_STATS
+// Measurement build only: out[2 s] = failed polls at wait site s (0 ready, 1 consumed,
+// 2 freed), out[2 s + 1] = waits that polled more than once.  reset != 0 zeroes them.
+extern "C" __attribute__((visibility("default"))) int enet_crc_debug_spin_stats(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(enet_crc::g_spin_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -3;
+  if (reset) {
+    static const unsigned long long zero[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_spin_stats), zero, sizeof(zero)) != hipSuccess) return -3;
+  }
+  return 0;
+}
+#endif
