@@ -59,4 +59,36 @@ ENET_HD int chunk_kind(const PacketGeo& g, uint32_t k, int32_t i, uint64_t base4
   return kChunkDirect;
 }
 
+// Lane geometry of crc32_uniform_lines_kernel (back-to-back packets of L = 16 n bytes from a
+// 128-B aligned base; group g of a round reads the round's lines [g L / 128, (g+1) L / 128)),
+// shared with its host model (tests/cpp/kernel_sim.cpp).  nsl = ceil(L / 128) slots per round.
+struct LinesLane {
+  int64_t off0;     // byte offset of this lane's slot-0 chunk from its round's start
+  bool dummy0;      // slot 0 reads the zero chunk (the group has NSL - 1 lines)
+  uint32_t am[2];   // slot s in {0, 1}: AND mask of the data words (0: chunk of packet g - 1)
+  uint32_t xm[2];   // slot s in {0, 1}: XOR into word 0 (the initial register)
+  bool keep[2];     // slot s in {0, 1}: keep the raw chunk for group g - 1
+  bool lo;          // takes a step-0 chunk from group g + 1
+  uint32_t src4;    // ds_bpermute byte address of that chunk's lane
+};
+
+ENET_HD LinesLane lines_lane(uint32_t L, int nsl, uint32_t g, uint32_t k) {
+  LinesLane r;
+  const uint32_t lg = g * L / 128u, lg1 = (g + 1u) * L / 128u;
+  const int first = nsl - (int)(lg1 - lg);  // 0 or 1
+  const uint32_t jg = (g * L % 128u) / 16u, j1 = ((g + 1u) * L % 128u) / 16u, j2 = ((g + 2u) * L % 128u) / 16u;
+  const uint32_t m = (j1 + 7u - k) & 7u;  // (j1 - 1 - k) mod 8
+  r.off0 = 128 * ((int64_t)lg1 - nsl) + 16 * (int64_t)m;
+  r.dummy0 = first == 1;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    r.am[s] = first == s && m < jg ? 0u : 0xFFFFFFFFu;
+    r.xm[s] = first == s && m == jg ? 0xFFFFFFFFu : 0u;
+    r.keep[s] = first == s;
+  }
+  r.lo = k < j1;
+  r.src4 = 4u * (g < 7u ? 8u * (g + 1u) + ((j2 + 8u - j1 + k) & 7u) : 8u * g + k);
+  return r;
+}
+
 }  // namespace enet_crc

@@ -1133,6 +1133,142 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 }
 
 // ---------------------------------------------------------------------------------
+// Uniform kernel, whole-line form: back-to-back packets (stride == length) whose length L
+// is a multiple of 16 from a 128-B aligned base, e.g. the G1 batch.  A round of 8 packets
+// is then 8L bytes = a whole number of 128-B lines starting on a line, and group g reads
+// the round's lines [Lg, Lg+1), Lg = floor(g L / 128): every line of the batch is read
+// once, whole, by one non-temporal DMA (the shape of tools/dma_probe P9, which streams
+// 1.26 GB in 193-200 us against 214-229 us for the register ring's loads, same calls).
+//   * Lane k of group g reads chunk m = (j1 - 1 - k) mod 8 of each of its lines, where
+//     j1 = ((g + 1) L mod 128) / 16 chunks of packet g lie in the next group's first line.
+//     Then the lane holds position k (chunk index from the packet end, mod 8) of every
+//     line, so the streams combine with the usual tree.  Slot s is line Lg+1 - NSL + s
+//     (NSL = ceil(L / 128)); a group with one line fewer reads the zero chunk in slot 0.
+//   * At the group's first line, chunks m < jg (jg = (g L mod 128) / 16) belong to packet
+//     g - 1: they are zeroed in the stream and kept; chunk m == jg is packet g's first
+//     (the initial register is XOR-ed into its first word).
+//   * After the round's slots, lane k < j1 takes its step-0 chunk, which group g + 1 kept,
+//     by ds_bpermute from lane (j2 - j1 + k) mod 8 of that group, and runs one more
+//     Horner step (the other lanes' last chunk was slot NSL - 1).
+// Same ring, waits, dispatch, combine and result batching as crc32_uniform_dma_kernel.  The
+// launch covers count / 8 whole rounds; launch_uniform sends the < 8 packets left to the
+// register kernel.
+// ---------------------------------------------------------------------------------
+#ifndef ENET_CRC_LINES_AUX
+#define ENET_CRC_LINES_AUX 2  // non-temporal (an A/B build may set 0: default cache policy)
+#endif
+
+template <int NSL>
+__global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  constexpr int R = kUniformRing;
+  static_assert(NSL >= R, "the ring reaches at most one round ahead");
+  __shared__ __attribute__((aligned(16))) UniformDmaLds<R> S;
+  uint32_t* const lds = S.tables;
+  auto& ring = S.ring;
+  constexpr int kLook = 2;
+  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kLook;
+  fill_lds(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(u.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t rounds = u.count / kPacketsPerWave;  // whole rounds only (launch contract)
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto round_of = [&](uint32_t d) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
+  const LinesLane ll = lines_lane(u.length, NSL, c.grp, c.k);
+  const uint64_t round_bytes = (uint64_t)kPacketsPerWave * u.length;
+  // This lane's slot-0 chunk in round rnd (rounds past the end re-read the last one).
+  auto lane_base = [&](uint64_t rnd) -> uint64_t {
+    return u.base + (rnd < rounds ? rnd : rounds - 1) * round_bytes + (uint64_t)ll.off0;
+  };
+  auto src_of = [&](uint64_t lb, int s) -> uint64_t {
+    return s == 0 && ll.dummy0 ? c.dummy : lb + (uint64_t)kBytesPerStep * (uint64_t)s;
+  };
+  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
+  auto dma = [&](uint64_t src, uint32_t q) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, ENET_CRC_LINES_AUX);
+  };
+
+  uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
+  if (rnd0 >= rounds) return;
+  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
+  {
+    const uint64_t lb = lane_base(rnd0);
+#pragma unroll
+    for (int f = 0; f < R; ++f) dma(src_of(lb, f), (uint32_t)f);
+  }
+  uint32_t q = 0;
+  u32x4 nextv = read_landed_slot<R - 1>(ring0 + lane * 16u);
+  uint32_t res = 0, j = 0;
+  uint64_t res_round = 0;
+  while (rnd0 < rounds) {
+    uint32_t d = 0;
+    if (lane == 0) d = lds_fetch_add_one(&S.next_dispatch);
+    const uint64_t lb = lane_base(rnd0), lbn = lane_base(rnd1);
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    u32x4 kept = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      const u32x4 v = nextv;
+      const int f = s + R;  // refill this slot's LDS slot R slots ahead
+      dma(f < NSL ? src_of(lb, f) : src_of(lbn, f - NSL), q);
+      q = q + 1 == (uint32_t)R ? 0u : q + 1;
+      const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
+      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+      if (s < 2) {  // the group's first line: slot 0, or slot 1 after a zero slot 0
+        if (ll.keep[s]) kept = v;
+        w0 = (w0 & ll.am[s]) ^ ll.xm[s];
+        w1 &= ll.am[s];
+        w2 &= ll.am[s];
+        w3 &= ll.am[s];
+      }
+      if (s == 0) {  // h = 0 on every lane: M32^32(0) = 0, no lookups
+        h0 = w0;
+        h1 = w1;
+        h2 = w2;
+        h3 = w3;
+        nextv = read_landed_slot<R - 1>(next_addr);
+      } else {
+        horner_step_and_read<R - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, nextv);
+      }
+      issue_order_fence();
+    }
+    // Step 0 of the lanes whose last chunk lies in the next group's first line.
+    {
+      const uint32_t a = ll.src4;
+      const uint32_t x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.x);
+      const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.y);
+      const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.z);
+      const uint32_t x3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.w);
+      const uint32_t s0 = horner_main(lds, h0, x0, c.lk), s1 = horner_main(lds, h1, x1, c.lk);
+      const uint32_t s2 = horner_main(lds, h2, x2, c.lk), s3 = horner_main(lds, h3, x3, c.lk);
+      h0 = ll.lo ? s0 : h0;
+      h1 = ll.lo ? s1 : h1;
+      h2 = ll.lo ? s2 : h2;
+      h3 = ll.lo ? s3 : h3;
+    }
+    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+    const uint32_t reg = finish_word(lds, y, 0u, c.lk);  // lane k == 0 holds the register
+    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    if (c.k == j) {
+      res = crc;
+      res_round = rnd0;
+    }
+    rnd0 = rnd1;
+    rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
+    if (j == 7u || rnd0 >= rounds) {
+      if (c.k <= j) out[res_round * kPacketsPerWave + c.grp] = res;
+      j = 0;
+    } else {
+      ++j;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the ring's last DMAs land before the wave's LDS goes away
+}
+
+// ---------------------------------------------------------------------------------
 // Ragged rounds on the LDS-DMA ring (crc32_ragged_jobs_kernel below).  Packets come
 // sorted by step class, so the 8 packets of a round need (nearly) the same number of
 // slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the packets with
@@ -1150,9 +1286,7 @@ struct RaggedRound {
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
   bool direct;          // top chunk read directly (not fallback / not before the packet)
   bool fast;            // wave-uniform: every lane's top is the same slot, no fallback, ns <= kRaggedFastMax
-  bool mixed;           // wave-uniform: not fast, but no fallback and ns <= kRaggedFastMax
   int32_t top_uniform;  // that slot (0 unless ns == kRaggedRing and the packets are shorter)
-  int32_t min_top;      // wave-uniform: the earliest top slot of the round's packets
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
@@ -1170,7 +1304,6 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   RaggedRound rr;
   const int32_t max_steps = wave_max_over_groups(nsteps);
   rr.ns = max(kRaggedRing, max_steps);
-  rr.min_top = rr.ns - max_steps;
   rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
   rr.top_slot = rr.ns - nsteps;
   // This lane's chunk at the top step, relative to top: chunk_offset(g, k, nsteps-1, top)
@@ -1194,7 +1327,6 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
   const bool fallback = __builtin_amdgcn_ballot_w64(rr.meta & kMetaFallback) != 0;
   rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform) && !fallback && rr.ns <= kRaggedFastMax;
-  rr.mixed = !rr.fast && !fallback && rr.ns <= kRaggedFastMax;
   return rr;
 }
 
@@ -1256,45 +1388,6 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
   }
 }
 
-// A round whose packets start at different slots (neighbouring step classes meet in a
-// sorted round) and that needs no fallback: the unrolled body of ragged_round_fast with
-// per-lane DMA sources (the zero chunk before each lane's top) and the top masking
-// applied on the slots where some lane has its top.  Every lane's register is 0 until
-// its top slot and reads zeros before it, so the round's first top slot (min_top) needs
-// no lookups and the slots before it are only consumed.
-template <int NS>
-__device__ __forceinline__ void ragged_round_mixed(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
-                                                   const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                                   uint32_t& h3) {
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const u32x4 v = R.nextv;
-    const int32_t f = s + kRaggedRing;
-    R.dma(f < NS ? ragged_src(cur, f, c.dummy) : ragged_src(nxt, f - NS, c.dummy));
-    if (s < cur.min_top) {
-      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
-      issue_order_fence();
-      continue;
-    }
-    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    if (s == NS - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
-    const bool top = s == cur.top_slot;
-    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
-      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
-    }
-    if (s == cur.min_top) {
-      h0 = w0;
-      h1 = w1;
-      h2 = w2;
-      h3 = w3;
-      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
-    } else {
-      horner_step_and_read<kRaggedRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, R.next_addr(), R.nextv);
-    }
-    issue_order_fence();
-  }
-}
-
 // Rounds of packets no longer than the ring (ns == kRaggedRing): top slot T = 0..ring-1.
 template <int... T>
 __device__ __forceinline__ bool ragged_round_short(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
@@ -1308,10 +1401,6 @@ template <int... I>
 __device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRound& cur, const RaggedRound& nxt,
                                                       RaggedRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                       uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
-  if (cur.mixed)
-    return ((ns == I + kRaggedRing ? (ragged_round_mixed<I + kRaggedRing>(cur, nxt, R, c, h0, h1, h2, h3), true)
-                                   : false) || ...) ||
-           (ns == kRaggedFastMax ? (ragged_round_mixed<kRaggedFastMax>(cur, nxt, R, c, h0, h1, h2, h3), true) : false);
   if (ns == kRaggedRing) return ragged_round_short(cur, nxt, R, c, h0, h1, h2, h3,
                                                    std::make_integer_sequence<int, kRaggedRing>{});
   return ((ns == I + kRaggedRing + 1 ? (ragged_round_fast<I + kRaggedRing + 1>(cur, nxt, R, c, h0, h1, h2, h3), true)
@@ -1365,7 +1454,7 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
 //     in HBM and cost one more launch).
 // Every LDS access after the first DMA is an asm statement with its own wait (hipcc would
 // order a plain LDS access behind the in-flight LDS-DMAs).  Same round bodies as
-// round 2's region kernel (ragged_round_fast / _mixed / _generic).
+// round 2's region kernel (ragged_round_fast / _generic).
 // ---------------------------------------------------------------------------------
 constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
 constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
@@ -1643,9 +1732,12 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
       }
     }
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    if (!(cur.fast || cur.mixed) ||
-        !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
-                               std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
+    // Rounds whose packets share a top slot take an unrolled body; the others (step
+    // classes meeting in a round, fallback chunks, long packets) the generic loop.  Unrolled
+    // bodies for the mixed rounds too made the kernel 143 KB instead of 59 KB and were no
+    // faster; the generic loop alone is 6 % slower.
+    if (!cur.fast || !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
+                                            std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
       ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
@@ -1754,6 +1846,30 @@ static hipError_t dispatch_uniform_regs(int ns, const UniformBatch& u, uint32_t*
   return e;
 }
 
+// crc32_uniform_lines_kernel's batches: back to back, 16-B multiple lengths, line-aligned base.
+static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length) {
+#ifdef ENET_CRC_NO_LINES  // A/B build: the register ring for these batches too
+  return false;
+#endif
+  return stride == length && (length & 15u) == 0 && (base & 127u) == 0;
+}
+
+template <int NSL>
+static hipError_t launch_uniform_lines(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
+  hipLaunchKernelGGL((crc32_uniform_lines_kernel<NSL>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  return hipGetLastError();
+}
+
+template <int... I>
+static hipError_t dispatch_uniform_lines(int nsl, const UniformBatch& u, uint32_t* out, hipStream_t stream,
+                                         unsigned blocks, std::integer_sequence<int, I...>) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((nsl == I + kUniformRing ? (e = launch_uniform_lines<I + kUniformRing>(u, out, stream, blocks), true)
+                                  : false) ||
+         ...);
+  return e;
+}
+
 // Aligned uniform batches (base and stride multiples of 4): packets up to kMaxRoundSteps
 // steps (<= 1792 B) run the register ring with line-split loads (the G1 path), packets of
 // >= 4 KiB the wave-per-packet kernel, the lengths in between the 8-packets-per-wave
@@ -1781,8 +1897,27 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
         hipLaunchKernelGGL((crc32_wave_dma_kernel<false>), dim3((unsigned)wblocks), dim3(kBlock), 0, stream, u, out);
       return hipGetLastError();
     }
-    if (nsx <= kMaxRoundSteps)
+    if (nsx <= kMaxRoundSteps) {
+      // Back-to-back 16-B-multiple packets from a line-aligned base: every line read once,
+      // whole, non-temporal (crc32_uniform_lines_kernel) for the whole rounds, the register
+      // ring for the < 8 packets left.
+      const int nsl = (int)((length + 127u) / 128u);
+      const uint64_t whole = count / kPacketsPerWave * kPacketsPerWave;
+      if (lines_shape(b0, stride, length) && nsl >= kUniformRing && nsl <= kMaxRoundSteps && whole > 0) {
+        const UniformBatch w{b0, stride, length, whole};
+        const unsigned wblocks = grid_for(whole, err);
+        if (err != hipSuccess) return err;
+        err = dispatch_uniform_lines(nsl, w, out, stream, wblocks,
+                                     std::make_integer_sequence<int, kMaxRoundSteps - kUniformRing + 1>{});
+        if (err != hipSuccess || whole == count) return err;
+        const UniformBatch t{b0 + whole * stride, stride, length, count - whole};
+        const unsigned tblocks = grid_for(count - whole, err);
+        if (err != hipSuccess) return err;
+        return dispatch_uniform_regs(nsx, t, out + whole, stream, tblocks,
+                                     std::make_integer_sequence<int, kMaxRoundSteps>{});
+      }
       return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
+    }
     if (nt_lines(u))
       hipLaunchKernelGGL((crc32_uniform_dma_kernel<true>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
     else

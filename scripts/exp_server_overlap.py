@@ -5,6 +5,7 @@ synchronize would wait for the server to exit (its 20-ms idle limit).
     ENET_CRC_AMD_LIB=rusty_enet_amd/lib/variants/libenet_crc_amd_testhooks.so python scripts/exp_server_overlap.py"""
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -47,9 +48,14 @@ for n in (1 << 19, 1 << 20):
                 else:
                     ctx.stop_server()
                 t = timed()
+                c0 = time.perf_counter()
                 if server:
-                    assert ctx([b"y"]) == rea.crc32([b"y"])  # still answering
-                print(f"n={n} rep={rep} server={'live' if server else 'none':4s} {rsv} CUs held back {t:8.1f} us",
-                      flush=True)
+                    got = ctx([b"y"])
+                call_us = (time.perf_counter() - c0) * 1e6
+                if server:
+                    assert got == rea.crc32([b"y"])
+                # a resident server answers in a few us; a relaunch after it exited costs ~20 us
+                print(f"n={n} rep={rep} server={'live' if server else 'none':4s} {rsv} CUs held back {t:8.1f} us"
+                      f"  next call {call_us:6.1f} us", flush=True)
 os.environ.pop("ENET_CRC_TEST_RESERVE")
 ctx.close()

@@ -13,6 +13,7 @@
 #include <random>
 #include <vector>
 
+#include "../../rusty_enet_amd/csrc/crc32_geometry.hpp"
 #include "../../rusty_enet_amd/csrc/crc32_ops.hpp"
 
 extern "C" {
@@ -85,6 +86,52 @@ static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
   return __builtin_bswap32(~reg);
 }
 
+// crc32_uniform_lines_kernel, lane by lane: one round of 8 back-to-back packets of L bytes
+// (L a multiple of 16) at the 128-B aligned offset r0; group g reads the round's lines
+// [g L / 128, (g+1) L / 128), lane k chunk m of each line (lines_lane, crc32_geometry.hpp).
+// Returns the number of wrong checksums; -1 if a lane would read outside the round.
+static int model_lines(const uint8_t* buf, uint64_t r0, uint32_t L) {
+  const int nsl = (int)((L + 127) / 128);
+  uint32_t h[64][4] = {}, kept[64][4] = {};
+  for (uint32_t lane = 0; lane < 64; ++lane) {
+    const LinesLane ll = lines_lane(L, nsl, lane / 8, lane % 8);
+    for (int s = 0; s < nsl; ++s) {
+      uint32_t w[4] = {0, 0, 0, 0};
+      if (!(s == 0 && ll.dummy0)) {
+        const int64_t off = ll.off0 + 128 * s;
+        if (off < 0 || off + 16 > 8 * (int64_t)L) return -1;
+        memcpy(w, buf + r0 + off, 16);
+      }
+      if (s < 2) {
+        if (ll.keep[s]) memcpy(kept[lane], w, 16);
+        w[0] = (w[0] & ll.am[s]) ^ ll.xm[s];
+        for (int j = 1; j < 4; ++j) w[j] &= ll.am[s];
+      }
+      for (int j = 0; j < 4; ++j) h[lane][j] = s == 0 ? w[j] : op(5, h[lane][j]) ^ w[j];
+    }
+  }
+  int bad = 0;
+  for (uint32_t g = 0; g < 8; ++g) {
+    uint32_t y[8];
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t lane = 8 * g + k;
+      const LinesLane ll = lines_lane(L, nsl, g, k);
+      uint32_t hh[4];
+      for (int j = 0; j < 4; ++j) hh[j] = ll.lo ? op(5, h[lane][j]) ^ kept[ll.src4 / 4][j] : h[lane][j];
+      y[k] = op(0, op(0, op(0, hh[0]) ^ hh[1]) ^ hh[2]) ^ hh[3];
+    }
+    for (int l = 1; l <= 3; ++l) {
+      const int d = 1 << (l - 1);
+      uint32_t t[8];
+      for (int k = 0; k < 8; ++k) t[k] = op(l + 1, y[k]);
+      for (int k = 0; k + d < 8; ++k) y[k] ^= t[k + d];
+    }
+    const uint32_t crc = __builtin_bswap32(~op(0, y[0]));
+    bad += crc != oracle_crc32(buf + r0 + g * L, L);
+  }
+  return bad;
+}
+
 int main() {
   int bad = 0;
   const uint32_t* ot = oracle_crc_table();
@@ -118,6 +165,17 @@ int main() {
       }
     }
     ++cases;
+  }
+  // The whole-line kernel: every 16-B multiple length it takes (5..14 lines per round slot).
+  for (uint32_t L = 528; L <= 1792; L += 16) {
+    for (int r = 0; r < 6; ++r) {
+      const int e = model_lines(buf.data(), 128 * (g() % 2048), L);
+      if (e != 0) {
+        if (bad < 10) printf("lines model L=%u: %d\n", L, e);
+        bad += e < 0 ? 1 : e;
+      }
+      ++cases;
+    }
   }
   printf("cases=%ld bad=%d\n", cases, bad);
   return bad ? 1 : 0;

@@ -289,6 +289,22 @@ def test_uniform_line_split_bases(dev, base_off):
         assert np.array_equal(got, want), (stride, length, base_off)
 
 
+@pytest.mark.parametrize("base_off", [0, 128, 384, 4096])
+def test_uniform_whole_lines_kernel(dev, base_off):
+    # Back-to-back packets of 16-B multiple lengths from a line-aligned base: the whole-line
+    # kernel (every line read once; group g's lines [g L / 128, (g+1) L / 128)) for every
+    # whole round, the register ring for the < 8 packets left.  Lengths 528..1792 (5..14
+    # lines per group slot), every j residue pattern, counts with and without a tail.
+    for length, n in [(528, 8), (528, 4099), (640, 3000), (1040, 1001), (1200, 8), (1200, 9), (1200, 4007),
+                      (1216, 777), (1280, 2048), (1392, 3007), (1504, 1600), (1776, 777), (1792, 1499)]:
+        data = splitmix64_bytes(base_off * 5 + length + n, base_off + n * length)
+        d = to_dev(data, dev)[base_off:]
+        assert d.data_ptr() % 128 == 0
+        got = as_u32(rea.crc32_batch(d, stride=length, length=length, count=n))
+        want = _oracle.crc32_uniform(data[base_off:], length, length, n, threads=8)
+        assert np.array_equal(got, want), (length, n, base_off, int(np.count_nonzero(got != want)))
+
+
 def test_long_packets_line_ends(dev):
     # Non-temporal DMAs need every packet to end on a 128-B line: ends aligned with the
     # starts aligned (64 KiB from an aligned base) or not (65536 - 128 from base + 128),
