@@ -1133,12 +1133,12 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 }
 
 // ---------------------------------------------------------------------------------
-// Uniform kernel, whole-line form: back-to-back packets (stride == length) whose length L
-// is a multiple of 16 from a 128-B aligned base, e.g. the G1 batch.  A round of 8 packets
-// is then 8L bytes = a whole number of 128-B lines starting on a line, and group g reads
-// the round's lines [Lg, Lg+1), Lg = floor(g L / 128): every line of the batch is read
-// once, whole, by one non-temporal DMA (the shape of tools/dma_probe P9, which streams
-// 1.26 GB in 193-200 us against 214-229 us for the register ring's loads, same calls).
+// Uniform kernel, whole-line form (the G1 path): back-to-back packets (stride == length)
+// whose length L is a multiple of 16 from a 128-B aligned base.  A round of 8 packets is
+// then 8L bytes = a whole number of 128-B lines starting on a line, and group g reads the
+// round's lines [Lg, Lg+1), Lg = floor(g L / 128): every line of the batch is read once,
+// whole, by one non-temporal load (the non-temporal hint pays only on lines read once; on a
+// line two packets share, the second read misses: tools/dma_probe P9).
 //   * Lane k of group g reads chunk m = (j1 - 1 - k) mod 8 of each of its lines, where
 //     j1 = ((g + 1) L mod 128) / 16 chunks of packet g lie in the next group's first line.
 //     Then the lane holds position k (chunk index from the packet end, mod 8) of every
@@ -1150,16 +1150,18 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 //   * After the round's slots, lane k < j1 takes its step-0 chunk, which group g + 1 kept,
 //     by ds_bpermute from lane (j2 - j1 + k) mod 8 of that group, and runs one more
 //     Horner step (the other lanes' last chunk was slot NSL - 1).
-// Same ring, waits, dispatch, combine and result batching as crc32_uniform_dma_kernel.  The
-// launch covers count / 8 whole rounds; launch_uniform sends the < 8 packets left to the
-// register kernel.
+// The launch covers count / 8 whole rounds; launch_uniform sends the < 8 packets left to
+// the register kernel.  Two forms: crc32_uniform_lines_kernel (the product) streams the
+// lines through a register ring like crc32_uniform_regs_kernel; crc32_uniform_lines_dma_kernel
+// (A/B builds only, -DENET_CRC_LINES_DMA) through the LDS-DMA ring of
+// crc32_uniform_dma_kernel.  Same lines, same lookups.
 // ---------------------------------------------------------------------------------
 #ifndef ENET_CRC_LINES_AUX
 #define ENET_CRC_LINES_AUX 2  // non-temporal (an A/B build may set 0: default cache policy)
 #endif
 
 template <int NSL>
-__global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void crc32_uniform_lines_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   constexpr int R = kUniformRing;
   static_assert(NSL >= R, "the ring reaches at most one round ahead");
   __shared__ __attribute__((aligned(16))) UniformDmaLds<R> S;
@@ -1266,6 +1268,108 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
     }
   }
   __builtin_amdgcn_s_waitcnt(0);  // the ring's last DMAs land before the wave's LDS goes away
+}
+
+typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4;
+
+template <int NSL>
+__global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) UniformRegsLds S;
+  uint32_t* const lds = S.tables;
+  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
+  fill_lds_regs(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(u.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t rounds = u.count / kPacketsPerWave;
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto round_of = [&](uint32_t d) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
+  const LinesLane ll = lines_lane(u.length, NSL, c.grp, c.k);
+  const uint64_t round_bytes = (uint64_t)kPacketsPerWave * u.length;
+  auto lane_base = [&](uint64_t rnd) -> uint64_t {
+    return u.base + (rnd < rounds ? rnd : rounds - 1) * round_bytes + (uint64_t)ll.off0;
+  };
+  auto ld = [&](uint64_t lb, int s) -> u32x4 {
+    const uint64_t a = s == 0 && ll.dummy0 ? c.dummy : lb + (uint64_t)kBytesPerStep * (uint64_t)s;
+    return __builtin_nontemporal_load(reinterpret_cast<GlobalU32x4*>(a));
+  };
+  uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
+  if (rnd0 >= rounds) return;
+  u32x4 q[NSL];
+  {
+    const uint64_t lb = lane_base(rnd0);
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      q[s] = ld(lb, s);
+      issue_order_fence();
+    }
+  }
+  uint32_t res = 0, j = 0;
+  uint64_t res_round = 0;
+  while (rnd0 < rounds) {
+    uint32_t d = 0;
+    if (lane == 0) d = atomicAdd(&S.next_dispatch, 1u);
+    const uint64_t lbn = lane_base(rnd1);
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    u32x4 kept = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      const u32x4 v = q[s];
+      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+      if (s < 2) {
+        if (ll.keep[s]) kept = v;
+        w0 = (w0 & ll.am[s]) ^ ll.xm[s];
+        w1 &= ll.am[s];
+        w2 &= ll.am[s];
+        w3 &= ll.am[s];
+      }
+      if (s == 0) {
+        h0 = w0;
+        h1 = w1;
+        h2 = w2;
+        h3 = w3;
+      } else {
+        h0 = horner_main(lds, h0, w0, c.lk);
+        h1 = horner_main(lds, h1, w1, c.lk);
+        h2 = horner_main(lds, h2, w2, c.lk);
+        h3 = horner_main(lds, h3, w3, c.lk);
+      }
+      issue_order_fence();
+      q[s] = ld(lbn, s);  // the next round's slot s
+      issue_order_fence();
+    }
+    {
+      const uint32_t a = ll.src4;
+      const uint32_t x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.x);
+      const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.y);
+      const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.z);
+      const uint32_t x3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.w);
+      const uint32_t s0 = horner_main(lds, h0, x0, c.lk), s1 = horner_main(lds, h1, x1, c.lk);
+      const uint32_t s2 = horner_main(lds, h2, x2, c.lk), s3 = horner_main(lds, h3, x3, c.lk);
+      h0 = ll.lo ? s0 : h0;
+      h1 = ll.lo ? s1 : h1;
+      h2 = ll.lo ? s2 : h2;
+      h3 = ll.lo ? s3 : h3;
+    }
+    const uint32_t y = combine_tree_rep(lds, h0, h1, h2, h3, c.lk);
+    const uint32_t reg = finish_word(lds, y, 0u, c.lk);
+    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
+    if (c.k == j) {
+      res = crc;
+      res_round = rnd0;
+    }
+    rnd0 = rnd1;
+    rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
+    if (j == 7u || rnd0 >= rounds) {
+      if (c.k <= j) out[res_round * kPacketsPerWave + c.grp] = res;
+      j = 0;
+    } else {
+      ++j;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1856,6 +1960,10 @@ static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length) {
 
 template <int NSL>
 static hipError_t launch_uniform_lines(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
+#ifdef ENET_CRC_LINES_DMA  // A/B build: the same lines through the LDS-DMA ring
+  hipLaunchKernelGGL((crc32_uniform_lines_dma_kernel<NSL>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
+  return hipGetLastError();
+#endif
   hipLaunchKernelGGL((crc32_uniform_lines_kernel<NSL>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }

@@ -1,7 +1,8 @@
 #!/usr/bin/env bash
-# A/B of the whole-line G1 kernel (default) against the register ring (nolines build) and
-# the whole-line kernel with plain DMAs (linesplain build): full GPU suite on the default
-# build first, then the uniform-shaped bench configs alternating, then rocprof stats.
+# A/B of the whole-line G1 kernel (default: register ring, non-temporal loads) against the
+# line-split register ring (nolines build) and the whole-line kernel on the LDS-DMA ring
+# (linesdma build): full GPU suite on the default build first, then the uniform bench
+# config alternating, then rocprof stats, FETCH_SIZE and counters of the default.
 #   gpurun --timeout 1200 -- bash scripts/gpu_r03_ab_lines.sh <tag>
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -15,7 +16,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
   > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
 tail -1 "$OUT/pytest_gpu.log"
 bash scripts/gpu_ab_configs.sh "$TAG" none "uniform" 4 rusty_enet_amd/lib/libenet_crc_amd.so \
-  $V/libenet_crc_amd_nolines.so $V/libenet_crc_amd_linesplain.so || exit $?
+  $V/libenet_crc_amd_nolines.so $V/libenet_crc_amd_linesdma.so || exit $?
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_uniform" -o run --output-format csv \

@@ -15,3 +15,6 @@ timeout -k 10 200 python scripts/exp_ragged_overhead.py --reps 30 > "$OUT/ragged
   || { tail -20 "$OUT/ragged_overhead.txt"; exit 1; }
 cat "$OUT/ragged_overhead.txt"
 bash scripts/gpu_g1_diff.sh "$TAG/g1diff"
+ENET_CRC_AMD_LIB="$ROOT/rusty_enet_amd/lib/variants/libenet_crc_amd_testhooks.so" timeout -k 10 170 \
+  python scripts/exp_server_overlap.py > "$OUT/server_overlap.txt" 2>&1 || { tail -20 "$OUT/server_overlap.txt"; exit 1; }
+cat "$OUT/server_overlap.txt"
