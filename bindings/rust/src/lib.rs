@@ -173,8 +173,8 @@ impl GpuCrc32 {
 
     /// How `crc32` moves one datagram: `ENET_CRC_PERCALL_ZEROCOPY` (default: one launch
     /// per call, nothing resident), `ENET_CRC_PERCALL_COPY`, or `ENET_CRC_PERCALL_PERSISTENT`
-    /// (opt-in: a server wave stays on the GPU while calls keep coming, holding one CU; a
-    /// device-wide synchronize waits for it until `stop_server` or its 20-ms idle exit).
+    /// (opt-in: a server wave stays on the GPU while calls keep coming; a device-wide
+    /// synchronize waits for it until `stop_server` or its 20-ms idle exit).
     /// None of them beats the CPU per datagram; batch instead.
     pub fn set_percall_mode(&self, mode: i32) -> Result<(), CrcError> {
         let st = unsafe { enet_crc_ctx_set_percall_mode(self.ctx.0, mode) };

@@ -62,13 +62,6 @@ int fail_hip(hipError_t e) {
 
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_cu_count[kMaxDevices];
-// Persistent per-call server waves that may be resident, per device, over every context
-// of the process.  Each holds one CU for up to 2 s, and the batch kernels' grids are sized
-// to one workgroup per CU with a static share each (a workgroup that finds its CU taken
-// would start only when another finishes, doubling the launch): the grids are sized to
-// the CUs left over instead (cu_count_for_current_device).
-std::atomic<int> g_live_servers[kMaxDevices];
-
 // Restores the caller's current device on scope exit.
 struct DeviceGuard {
   int prev = -1;
@@ -120,11 +113,13 @@ hipError_t device_slot_ladder(const uint32_t** out) {
   return hipSuccess;
 }
 
-// CUs a batch launch on the current device may count on: all of them, minus one per XCD
-// for each persistent server wave that may be resident there (g_live_servers).  The
-// dispatcher deals workgroups to the 8 XCDs round-robin, so with 255 workgroups the
-// XCD that hosts the server would get 32 workgroups for its 31 free CUs and one of them
-// would start only when another finishes (measured: +15 % on a G2-shaped batch).
+// CUs a batch launch on the current device sizes its grid to: all of them, also while a
+// persistent per-call server wave (ENET_CRC_PERCALL_PERSISTENT) is resident.  Measured
+// (profiles/r03/s1/server_overlap*.txt, 3 interleaved repetitions, 512K and 1M G2-shaped
+// packets): with a live server, full grids ran at the no-server time (86.4-89.5 us vs
+// 88.2-88.5; 173.8-186.8 vs 172.8-182.9), while holding one CU per XCD back made every
+// launch 6-10 % slower (94.6-99.1; 183.4-190.0) -- the reserve of round 3's first session
+// was removed.
 int cu_count_for_current_device() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
@@ -133,14 +128,15 @@ int cu_count_for_current_device() {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
     g_cu_count[dev].store(n, std::memory_order_relaxed);
   }
-  constexpr int kXcds = 8;
-  const int live = g_live_servers[dev].load(std::memory_order_acquire);
-  int reserve = kXcds * live;
 #ifdef ENET_CRC_TEST_HOOKS
-  // Test build only: ENET_CRC_TEST_RESERVE=n holds back n CUs whether or not a server runs.
-  if (const char* v = getenv("ENET_CRC_TEST_RESERVE")) reserve = atoi(v);
+  // Test build only: ENET_CRC_TEST_RESERVE=n holds back n CUs (scripts/exp_server_overlap.py).
+  constexpr int kXcds = 8;
+  if (const char* v = getenv("ENET_CRC_TEST_RESERVE")) {
+    const int reserve = atoi(v);
+    return n - reserve >= kXcds ? n - reserve : kXcds;
+  }
 #endif
-  return n - reserve >= kXcds ? n - reserve : kXcds;
+  return n;
 }
 
 
@@ -230,17 +226,12 @@ struct PerCall {
   bool req_vram = false;      // request mailbox in device memory written through the BAR
   hipStream_t mb_stream = nullptr;
   int mb_device = 0;          // device of mb_stream (lane 0's)
-  bool mb_launched = false;   // a server was launched and may still run (counted in g_live_servers)
+  bool mb_launched = false;   // a server was launched and may still run
   uint32_t mb_seq = 0;        // last request number posted
 };
 
-// The only writer of PerCall::mb_launched: keeps g_live_servers in step with it.
-void set_server_live(PerCall& c, bool live) {
-  if (live == c.mb_launched) return;
-  c.mb_launched = live;
-  if (c.mb_device >= 0 && c.mb_device < kMaxDevices)
-    g_live_servers[c.mb_device].fetch_add(live ? 1 : -1, std::memory_order_acq_rel);
-}
+// The only writer of PerCall::mb_launched.
+void set_server_live(PerCall& c, bool live) { c.mb_launched = live; }
 
 // A worker thread bound to one lane: runs one job at a time for the calling thread.
 class Worker {
