@@ -1393,10 +1393,7 @@ struct RaggedRound {
   int32_t top_uniform;  // that slot (0 unless ns == kRaggedRing and the packets are shorter)
 };
 
-constexpr int kRaggedFastMax = 14;
-#ifndef ENET_CRC_RAGGED_NT
-#define ENET_CRC_RAGGED_NT 0  // A/B builds: 1 = non-temporal DMAs for a packet's inner pieces
-#endif  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
+constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
 
 // Per-lane round state from the group's packet record (ragged_record's fields; an invalid
 // group -- past the batch, or a re-read record -- is an empty packet at base4).  Every
