@@ -1276,9 +1276,6 @@ template <int NSL>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
-  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
-  fill_lds_regs(lds);
-  __syncthreads();
   const LaneConsts c = lane_consts(u.base);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1297,8 +1294,11 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
     return __builtin_nontemporal_load(reinterpret_cast<GlobalU32x4*>(a));
   };
   uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
-  if (rnd0 >= rounds) return;
   u32x4 q[NSL];
+  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
+  fill_lds_regs(lds);
+  __syncthreads();
+  if (rnd0 >= rounds) return;
   {
     const uint64_t lb = lane_base(rnd0);
 #pragma unroll
