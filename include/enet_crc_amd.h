@@ -80,8 +80,9 @@ typedef struct enet_crc_ctx enet_crc_ctx;
  * (device memory the host writes through the PCIe BAR on large-BAR devices, else pinned
  * host memory; answers in pinned host memory): no kernel launch per call (~3.4 us).
  * Datagrams above 4096 B take the zero-copy path.  While it runs:
- *   - batch launches on that device keep their full grids: measured, they run at their
- *     no-server time next to it (holding a CU back for it cost 6-10 %);
+ *   - any batch launch on that device (any context, the context-free *_device entry points,
+ *     rings) sends it home first: it exits at its next poll, so the batch gets every CU, and
+ *     the next per-call call relaunches it (one launch, ~20-40 us);
  *   - a device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize())
  *     waits for it: it exits 20 ms after the last call, or at once on
  *     enet_crc_ctx_stop_server(), a mode change, a batch entry of the same context or

@@ -59,6 +59,12 @@ namespace enet_crc {
 __device__ const OpTables g_op_tables = kOpTables;
 // Read by every lane whose chunk lies outside its packet; never written.
 __device__ __attribute__((aligned(64))) const uint32_t g_zero_chunk[64] = {0};
+// The device's per-call server kick word (enet_crc_abi.hip, crc32_mailbox.hpp), or null.
+__device__ uint32_t* g_kick_word = nullptr;
+
+hipError_t set_device_kick_word(uint32_t* d_word) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_kick_word), &d_word, sizeof(d_word));
+}
 
 namespace {
 
@@ -81,6 +87,20 @@ constexpr int kStreamDepth = 8;  // ring depth of the streaming kernel
 
 __device__ __forceinline__ uint32_t load_word(uint64_t addr) { return *reinterpret_cast<GlobalU32*>(addr); }
 __device__ __forceinline__ u32x4 load_chunk(uint64_t addr) { return reinterpret_cast<GlobalU32x4A4*>(addr)->v; }
+
+// A batch kernel's first thread bumps the device's kick word: a resident per-call server
+// wave exits at its next poll and frees its CU for this grid (one workgroup per CU with a
+// static share: a workgroup left waiting for that CU would double the launch).  Vector
+// load and store with system scope, waited for at once (no scalar-cache writes).
+__device__ __forceinline__ void send_servers_home() {
+  if (blockIdx.x != 0 || threadIdx.x != 0 || gridDim.x == 1) return;
+  uint32_t* const k = g_kick_word;
+  if (!k) return;
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(k) : "memory");
+  v += 1u;
+  asm volatile("global_store_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : : "v"(k), "v"(v) : "memory");
+}
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -286,6 +306,37 @@ __device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32
   return y;
 }
 
+// The ragged jobs kernel's tables: fill_lds's, plus M32^2 and M32^12 (kJobsM2Dword).
+__device__ __forceinline__ void fill_lds_jobs(uint32_t* lds) {
+  fill_lds(lds);
+  for (int x = threadIdx.x; x < 1024; x += kBlock) {
+    lds[kJobsM2Dword + x] = g_op_tables.op[1][x >> 8][x & 255];
+    lds[kJobsM12Dword + x] = g_op_tables.m12[x >> 8][x & 255];
+  }
+}
+
+// combine_tree in 4 dependent LDS round trips instead of 6 (the ragged jobs kernel, whose
+// per-round overhead is mostly such round trips): in-lane a = M h0 ^ h1 and b = M h2 ^ h3
+// side by side, then y = M^2 a ^ b; across the group a radix-4 tree: lane k = 4i + q applies
+// M^(4q) (q = 1, 2, 3: M^4, M^8, M^12), lanes 4i gather their quad by DPP, lane 4 applies
+// M^16 and lane 0 adds it.  The result equals combine_tree's: sum over k of M^(4k) y_k.
+__device__ __forceinline__ uint32_t combine_tree_jobs(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
+                                                     uint32_t h3, const Lookup& lk) {
+  const uint32_t a = apply_rep(lds, h0, h1, lk.lp1, lk);
+  const uint32_t b = apply_rep(lds, h2, h3, lk.lp1, lk);
+  uint32_t y = apply_small(lds + kJobsM2Dword, a) ^ b;
+  const uint32_t k = threadIdx.x & (G - 1), q = k & 3u;
+  uint32_t t = y;
+  if (q != 0) {
+    const uint32_t set = q == 1 ? kTreeDword : (q == 2 ? kTreeDword + 1024 : kJobsM12Dword);
+    t = apply_small(lds + set, y);
+  }
+  y = t ^ from_lane_plus<1>(t) ^ from_lane_plus<2>(t) ^ from_lane_plus<3>(t);  // valid on lanes 4i
+  uint32_t u = 0;
+  if (k == 4u) u = apply_small(lds + kTreeDword + 2048, y);  // M32^16
+  return y ^ from_lane_plus<4>(u);
+}
+
 __device__ __forceinline__ void fill_lds_regs(uint32_t* lds) {
   fill_replicated(lds, kMainLevel);
   fill_replicated(lds + kTreeRepDword, 2, 3);
@@ -390,6 +441,7 @@ __device__ __forceinline__ uint64_t slot_addr(const RoundPlan<NS>& pl, int s, ui
 
 template <int NS, bool kRagged>
 __global__ __launch_bounds__(kBlock) void crc32_rounds_kernel(Batch<kRagged> b, uint32_t* __restrict__ out) {
+  send_servers_home();
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   fill_lds(lds);
   __syncthreads();
@@ -520,6 +572,7 @@ __device__ __forceinline__ void stream_rounds(const uint32_t* lds, const Batch<k
 
 template <int U, bool kRagged>
 __global__ __launch_bounds__(kBlock) void crc32_stream_kernel(Batch<kRagged> b, uint32_t* __restrict__ out) {
+  send_servers_home();
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsDwords];
   fill_lds(lds);
   __syncthreads();
@@ -718,6 +771,7 @@ __device__ __forceinline__ uint32_t lds_fetch_add_one(uint32_t* counter) {
 // 1.26 GB; on lines a packet shares with its neighbour the hint costs a second fetch).
 template <bool kNT>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  send_servers_home();
   constexpr int kDmaRing = kUniformRing;
   __shared__ __attribute__((aligned(16))) UniformDmaLds<kDmaRing> S;
   uint32_t* const lds = S.tables;
@@ -905,6 +959,7 @@ __device__ __forceinline__ uint32_t combine_wave(const uint32_t* lds, uint32_t h
 
 template <bool kNT>
 __global__ __launch_bounds__(kBlock) void crc32_wave_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  send_servers_home();
   constexpr int kDmaRing = kWaveRing;
   __shared__ __attribute__((aligned(16))) WaveDmaLds S;
   uint32_t* const lds = S.tables;
@@ -1022,6 +1077,7 @@ struct UniformRegsLds {
 
 template <int NS>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  send_servers_home();
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
@@ -1162,6 +1218,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 
 template <int NSL>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  send_servers_home();
   constexpr int R = kUniformRing;
   static_assert(NSL >= R, "the ring reaches at most one round ahead");
   __shared__ __attribute__((aligned(16))) UniformDmaLds<R> S;
@@ -1274,6 +1331,7 @@ typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4;
 
 template <int NSL>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  send_servers_home();
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
   const LaneConsts c = lane_consts(u.base);
@@ -1563,7 +1621,7 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
 constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
 constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
 #ifndef ENET_CRC_JOB_SLOTS
-#define ENET_CRC_JOB_SLOTS 8
+#define ENET_CRC_JOB_SLOTS 6
 #endif
 constexpr int kJobSlots = ENET_CRC_JOB_SLOTS;                    // job slots in LDS
 constexpr int kJobAhead = 2;                                     // jobs built ahead of the one claimed
@@ -1580,7 +1638,7 @@ struct JobSlot {
   uint32_t res[kJobPackets];
 };
 struct RaggedJobsLds {
-  uint32_t tables[kLdsDwords];
+  uint32_t tables[kJobsLdsDwords];
   u32x4 ring[kRaggedRing][kWavesPerBlock][64];
   JobSlot job[kJobSlots];
   uint32_t ready[kJobSlots];     // k + 1 once the workgroup's k-th job has its records here
@@ -1605,11 +1663,6 @@ __device__ __forceinline__ uint32_t lds_ld32(uint32_t a) {
   asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
   return v;
 }
-__device__ __forceinline__ uint64_t lds_ld64(uint32_t a) {
-  uint64_t v;
-  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-  return v;
-}
 __device__ __forceinline__ u32x4 lds_ld128(uint32_t a) {
   u32x4 v;
   asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
@@ -1617,6 +1670,9 @@ __device__ __forceinline__ u32x4 lds_ld128(uint32_t a) {
 }
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
   asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st32_nowait(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 __device__ __forceinline__ void lds_st64(uint32_t a, uint64_t v) {
   asm volatile("ds_write_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(a), "v"(v) : "memory");
@@ -1632,31 +1688,25 @@ __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
-#ifdef ENET_CRC_SPIN_STATS
-// Measurement build only (make variant NAME=spin DEFS=-DENET_CRC_SPIN_STATS): failed polls
-// and waits per wait site, read back with enet_crc_debug_spin_stats.
-__device__ unsigned long long g_spin_stats[8];
+#ifdef ENET_CRC_ROUND_STAMPS
+// Measurement build only (make variant NAME=stamps DEFS=-DENET_CRC_ROUND_STAMPS): per-wave
+// s_memtime sums of the ragged jobs kernel, read back with enet_crc_debug_round_stamps:
+// [0] round bodies, [1] the whole round loop, [2] rounds, [3] job builds, [4] combine and
+// finish, [5] the next round's record read and plan (make_round).
+__device__ unsigned long long g_round_stamps[8];
 #endif
 
 // Spin (asleep) until the LDS word at `a` equals `want`; false after kJobSpinLimit polls.
-template <int kSite = 0>
 __device__ __forceinline__ bool lds_wait_eq(uint32_t a, uint32_t want) {
   for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
-    if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) {
-#ifdef ENET_CRC_SPIN_STATS
-      if ((threadIdx.x & 63u) == 0) {
-        atomicAdd(&g_spin_stats[2 * kSite], (unsigned long long)i);
-        atomicAdd(&g_spin_stats[2 * kSite + 1], i ? 1ull : 0ull);
-      }
-#endif
-      return true;
-    }
+    if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) return true;
     __builtin_amdgcn_s_sleep(2);
   }
   return false;
 }
 
 __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
+  send_servers_home();
   constexpr int kDmaRing = kRaggedRing;
   __shared__ __attribute__((aligned(16))) RaggedJobsLds S;
   uint32_t* const lds = S.tables;
@@ -1668,7 +1718,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     S.freed[threadIdx.x] = 0;
   }
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kLook;
-  fill_lds(lds);
+  fill_lds_jobs(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1793,13 +1843,15 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     const uint32_t k = d / RJ, slot = k % kJobSlots;
     bool rv = round_valid(d);
     if (rv && k + 1u > seen_ready) {
-      rv = lds_wait_eq<0>(lds_addr(&S.ready[slot]), k + 1u);
+      rv = lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u);
       if (rv) seen_ready = k + 1u;
     }
     if (rv) {
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d % RJ) * kJobRoundBytes;
-      ax = lds_ld64(r + 8u * c.grp);
-      info = lds_ld32(r + 64u + 4u * c.grp);
+      asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"  // one round trip
+                   : "=&v"(ax), "=&v"(info)
+                   : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp)
+                   : "memory");
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
     }
     return round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
@@ -1817,6 +1869,10 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
 #pragma unroll
   for (int f = 0; f < kDmaRing; ++f) R.dma(ragged_src(cur, f, c.dummy));  // cur.ns >= kDmaRing
   R.nextv = read_landed_slot<kDmaRing - 1>(R.next_addr());
+#ifdef ENET_CRC_ROUND_STAMPS
+  uint64_t st_body = 0, st_build = 0, st_rounds = 0, st_comb = 0, st_make = 0;
+  const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
+#endif
   while (round_valid(rnd0)) {
     uint32_t d = 0;
     if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
@@ -1829,13 +1885,16 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     bool build = false;
     const uint32_t kb = d / RJ + kJobAhead, bslot = kb % kJobSlots;
     if (d % RJ == 0 && kb >= first_jobs && job_of(kb) < b.njobs) {
-      build = kb < (uint32_t)kJobSlots || lds_wait_eq<1>(lds_addr(&S.consumed[bslot]), RJ);
+      build = kb < (uint32_t)kJobSlots || lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ);
       if (build) {
         if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
         job_dma(job_of(kb), bslot);
       }
     }
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+#ifdef ENET_CRC_ROUND_STAMPS
+    const uint64_t st_b0 = __builtin_amdgcn_s_memtime();
+#endif
     // Rounds whose packets share a top slot take an unrolled body; the others (step
     // classes meeting in a round, fallback chunks, long packets) the generic loop.  Unrolled
     // bodies for the mixed rounds too made the kernel 143 KB instead of 59 KB and were no
@@ -1843,17 +1902,28 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     if (!cur.fast || !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
                                             std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
       ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
-    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+#ifdef ENET_CRC_ROUND_STAMPS
+    const uint64_t st_b1 = __builtin_amdgcn_s_memtime();
+    st_body += st_b1 - st_b0;
+    ++st_rounds;
+#endif
+    const uint32_t y = combine_tree_jobs(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
+#ifdef ENET_CRC_ROUND_STAMPS
+    reg = __builtin_amdgcn_readfirstlane(reg) == 0x12345678u ? reg + 1u : reg;  // the combine ends here
+    st_comb += __builtin_amdgcn_s_memtime() - st_b1;
+#endif
     // The round's checksums into the job's result array; the last round of a job
     // writes the job's checksums to HBM.
     const uint32_t k0 = rnd0 / RJ, slot0 = k0 % kJobSlots;
     if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
-      if (lds_wait_eq<2>(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u))
+      if (lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
     }
-    if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
+    // The checksum store is not waited for on its own: the done counter's wait below covers
+    // it (LDS operations complete in order).
+    if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32_nowait(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
     old = __builtin_amdgcn_readfirstlane(old);
@@ -1874,13 +1944,35 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
         lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
       }
     }
+#ifdef ENET_CRC_ROUND_STAMPS
+    const uint64_t st_j0 = __builtin_amdgcn_s_memtime();
+#endif
     if (build) job_build(job_of(kb), bslot, kb + 1u);
+#ifdef ENET_CRC_ROUND_STAMPS
+    st_build += __builtin_amdgcn_s_memtime() - st_j0;
+#endif
+#ifdef ENET_CRC_ROUND_STAMPS
+    const uint64_t st_m0 = __builtin_amdgcn_s_memtime();
+#endif
     const RaggedRound after = make_round(d);
+#ifdef ENET_CRC_ROUND_STAMPS
+    st_make += __builtin_amdgcn_s_memtime() - st_m0 + (after.id == 0x7FFFFFFFu ? 1u : 0u);
+#endif
     rnd0 = rnd1;
     rnd1 = d;
     cur = nxt;
     nxt = after;
   }
+#ifdef ENET_CRC_ROUND_STAMPS
+  if (lane == 0) {
+    atomicAdd(&g_round_stamps[0], (unsigned long long)st_body);
+    atomicAdd(&g_round_stamps[1], (unsigned long long)(__builtin_amdgcn_s_memtime() - st_t0));
+    atomicAdd(&g_round_stamps[2], (unsigned long long)st_rounds);
+    atomicAdd(&g_round_stamps[3], (unsigned long long)st_build);
+    atomicAdd(&g_round_stamps[4], (unsigned long long)st_comb);
+    atomicAdd(&g_round_stamps[5], (unsigned long long)st_make);
+  }
+#endif
   __builtin_amdgcn_s_waitcnt(0);
 }
 
@@ -2090,15 +2182,14 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
 
 }  // namespace enet_crc
 
-#ifdef ENET_CRC_SPIN_STATS
-// Measurement build only: out[2 s] = failed polls at wait site s (0 ready, 1 consumed,
-// 2 freed), out[2 s + 1] = waits that polled more than once.  reset != 0 zeroes them.
-extern "C" __attribute__((visibility("default"))) int enet_crc_debug_spin_stats(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(enet_crc::g_spin_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+#ifdef ENET_CRC_ROUND_STAMPS
+// Measurement build only: g_round_stamps (see its definition); reset != 0 zeroes them.
+extern "C" __attribute__((visibility("default"))) int enet_crc_debug_round_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(enet_crc::g_round_stamps), sizeof(unsigned long long) * 8) != hipSuccess)
     return -3;
   if (reset) {
     static const unsigned long long zero[8] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_spin_stats), zero, sizeof(zero)) != hipSuccess) return -3;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_round_stamps), zero, sizeof(zero)) != hipSuccess) return -3;
   }
   return 0;
 }

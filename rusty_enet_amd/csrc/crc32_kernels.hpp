@@ -35,4 +35,7 @@ hipError_t device_slot_ladder(const uint32_t** out);
 // Cached hipDeviceAttributeMultiprocessorCount of the calling thread's device.
 int cu_count_for_current_device();
 
+// Registers the current device's kick word (enet_crc_abi.hip) with its batch kernels.
+hipError_t set_device_kick_word(uint32_t* d_word);
+
 }  // namespace enet_crc

@@ -49,14 +49,17 @@ __device__ __forceinline__ void sys_load64(const uint8_t* p, u32x4m& a, u32x4m& 
       : "memory");
 }
 
-// Two adjacent words in one load (the host writes them with one 64-bit store).
-__device__ __forceinline__ void sys_load2(const uint32_t* p, uint32_t& lo, uint32_t& hi) {
+// Two adjacent words in one load (the host writes them with one 64-bit store), and the
+// device's kick word, both in flight before one wait.
+__device__ __forceinline__ void sys_load2_kick(const uint32_t* p, const uint32_t* kick, uint32_t& lo, uint32_t& hi,
+                                               uint32_t& k) {
   uint64_t v;
   asm volatile(
-      "global_load_dwordx2 %0, %1, off sc0 sc1\n\t"
+      "global_load_dwordx2 %0, %2, off sc0 sc1\n\t"
+      "global_load_dword %1, %3, off sc0 sc1\n\t"
       "s_waitcnt vmcnt(0)"
-      : "=v"(v)
-      : "v"(p)
+      : "=&v"(v), "=&v"(k)
+      : "v"(p), "v"(kick)
       : "memory");
   lo = (uint32_t)v;
   hi = (uint32_t)(v >> 32);
@@ -86,7 +89,7 @@ __device__ __forceinline__ uint32_t from_lane_down(uint32_t v) {
 }
 
 __global__ __launch_bounds__(64) void crc32_mailbox_kernel(const Mailbox* req, Mailbox* resp,
-                                                           const uint32_t* __restrict__ ladder) {
+                                                           const uint32_t* __restrict__ ladder, const uint32_t* kick) {
   __shared__ uint32_t m32[kSlotLevelDwords];               // ladder level 0: M32
   __shared__ uint32_t m32x2[kSlotLevelDwords];             // ladder level 1: M32^2
   __shared__ uint32_t m32x4[kSlotLevelDwords];             // ladder level 2: M32^4
@@ -101,14 +104,16 @@ __global__ __launch_bounds__(64) void crc32_mailbox_kernel(const Mailbox* req, M
   }
   __syncthreads();
   uint32_t last = __builtin_amdgcn_readfirstlane(sys_load(&resp->done));
+  const uint32_t kick0 = __builtin_amdgcn_readfirstlane(sys_load(kick));
   const uint64_t t0 = wall_clock64();
   uint64_t t_last = t0;
   for (;;) {
-    uint32_t seq, len;
-    sys_load2(&req->seq, seq, len);  // one 64-bit word: the host posts both with one store
+    uint32_t seq, len, k;
+    sys_load2_kick(&req->seq, kick, seq, len, k);  // seq and len: one 64-bit word, posted with one store
     seq = __builtin_amdgcn_readfirstlane(seq);
     len = __builtin_amdgcn_readfirstlane(len);
-    if (seq == kMailboxStop) break;
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (seq == kMailboxStop || k != kick0) break;  // stop request, or a batch launch wants the CU
     const uint64_t now = wall_clock64();
 #ifdef ENET_CRC_TEST_HOOKS
     // Test build only: a 4095-byte request is never answered (the host's timeout path).
@@ -166,8 +171,9 @@ __global__ __launch_bounds__(64) void crc32_mailbox_kernel(const Mailbox* req, M
 
 }  // namespace
 
-hipError_t launch_mailbox(const Mailbox* req, Mailbox* resp, const uint32_t* ladder, hipStream_t stream) {
-  hipLaunchKernelGGL(crc32_mailbox_kernel, dim3(1), dim3(64), 0, stream, req, resp, ladder);
+hipError_t launch_mailbox(const Mailbox* req, Mailbox* resp, const uint32_t* ladder, const uint32_t* kick,
+                          hipStream_t stream) {
+  hipLaunchKernelGGL(crc32_mailbox_kernel, dim3(1), dim3(64), 0, stream, req, resp, ladder, kick);
   return hipGetLastError();
 }
 

@@ -34,7 +34,12 @@ struct alignas(128) Mailbox {
 // through the PCIe BAR when the device has a large BAR, else pinned host memory), `resp`
 // that of the one the answers go to (done, result: always pinned host memory, where the
 // host polls); `ladder` is the device ladder of crc32_slot.hpp.  The kernel returns on
-// kMailboxStop, after kMailboxIdleTicks without a request, or after kMailboxMaxTicks.
-hipError_t launch_mailbox(const Mailbox* req, Mailbox* resp, const uint32_t* ladder, hipStream_t stream);
+// kMailboxStop, after kMailboxIdleTicks without a request, after kMailboxMaxTicks, or when
+// the device's kick word changes.
+// `kick` is the device's kick word (enet_crc_abi.hip): the first workgroup of every batch
+// kernel on the device bumps it, and the server exits as soon as it reads another value than
+// at its start, so the CU it holds is free for the batch's grid.
+hipError_t launch_mailbox(const Mailbox* req, Mailbox* resp, const uint32_t* ladder, const uint32_t* kick,
+                          hipStream_t stream);
 
 }  // namespace enet_crc

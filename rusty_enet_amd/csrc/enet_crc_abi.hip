@@ -113,13 +113,49 @@ hipError_t device_slot_ladder(const uint32_t** out) {
   return hipSuccess;
 }
 
-// CUs a batch launch on the current device sizes its grid to: all of them, also while a
-// persistent per-call server wave (ENET_CRC_PERCALL_PERSISTENT) is resident.  Measured
-// (profiles/r03/s1/server_overlap*.txt, 3 interleaved repetitions, 512K and 1M G2-shaped
-// packets): with a live server, full grids ran at the no-server time (86.4-89.5 us vs
-// 88.2-88.5; 173.8-186.8 vs 172.8-182.9), while holding one CU per XCD back made every
-// launch 6-10 % slower (94.6-99.1; 183.4-190.0) -- the reserve of round 3's first session
-// was removed.
+// Each device's kick word (ENET_CRC_PERCALL_PERSISTENT).  A resident per-call server wave
+// holds a CU, and the batch kernels size their grids to one workgroup per CU with a static
+// share each: measured next to an answering server, a G2-shaped batch took 141-149 us
+// instead of ~88 (profiles/r03/s3, s4/server_latency.txt) -- one workgroup waited for a
+// whole share -- and holding CUs back for it instead cost 6-10 % (server_overlap.txt).  So
+// the first workgroup of every batch kernel bumps the word as it starts
+// (send_servers_home, crc32_kernels.hip); a server exits as soon as it reads another value
+// than at its start, and the next per-call call relaunches it.
+std::atomic<uint32_t*> g_kick_dev[kMaxDevices];  // device address of the word
+std::mutex g_kick_lock;
+
+// The kick word of `dev` (allocated on first use: fine-grained device memory, or mapped
+// pinned host memory when the device's memory is not host-visible), registered with the
+// batch kernels of that device.
+hipError_t kick_word(int dev, uint32_t** dev_ptr) {
+  if (!g_kick_dev[dev].load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> lk(g_kick_lock);
+    if (!g_kick_dev[dev].load(std::memory_order_relaxed)) {
+      DeviceGuard g(dev);
+      uint32_t* d = nullptr;
+      if (hipExtMallocWithFlags((void**)&d, 128, hipDeviceMallocFinegrained) == hipSuccess) {
+        hipError_t e = hipMemset(d, 0, 128);
+        if (e != hipSuccess) return e;
+      } else {
+        (void)hipGetLastError();
+        uint32_t* h = nullptr;
+        hipError_t e = hipHostMalloc((void**)&h, 128, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return e;
+        memset(h, 0, 128);
+        e = hipHostGetDevicePointer((void**)&d, h, 0);
+        if (e != hipSuccess) return e;
+      }
+      const hipError_t e = set_device_kick_word(d);
+      if (e != hipSuccess) return e;
+      g_kick_dev[dev].store(d, std::memory_order_release);
+    }
+  }
+  *dev_ptr = g_kick_dev[dev].load(std::memory_order_acquire);
+  return hipSuccess;
+}
+
+// CUs a batch launch on the current device sizes its grid to: all of them (a resident
+// per-call server is sent home by the kernel itself, see g_kick_dev).
 int cu_count_for_current_device() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
@@ -734,8 +770,10 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
     if (c.req_vram) __builtin_ia32_sfence();
     __atomic_store_n(reinterpret_cast<uint64_t*>(&c.req->seq), ((uint64_t)total << 32) | seq, __ATOMIC_RELEASE);
     if (c.req_vram) __builtin_ia32_sfence();
+    uint32_t* kick = nullptr;
+    ENET_HIP_TRY(kick_word(c.mb_device, &kick));
     auto launch = [&]() -> hipError_t {
-      const hipError_t e = launch_mailbox(c.d_req, c.d_mb, ladder, c.mb_stream);
+      const hipError_t e = launch_mailbox(c.d_req, c.d_mb, ladder, kick, c.mb_stream);
       set_server_live(c, e == hipSuccess);
       return e;
     };

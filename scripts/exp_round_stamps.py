@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Experiment (measurement build, make variant NAME=spin DEFS=-DENET_CRC_SPIN_STATS): how
-long the ragged jobs kernel's waves poll its three LDS job flags (ready, consumed, freed)
-per launch, on G2, the fragmented 64-KiB payloads and equal-length ragged batches.
-    ENET_CRC_AMD_LIB=rusty_enet_amd/lib/variants/libenet_crc_amd_spin.so python scripts/exp_spin_stats.py
+"""Experiment (measurement build, make variant NAME=stamps DEFS=-DENET_CRC_ROUND_STAMPS): where
+the ragged jobs kernel's waves spend their time -- s_memtime sums per wave of the round
+bodies (the slots), the job builds and the whole round loop; the rest is the per-round
+bookkeeping (record read and plan, combine, result, flags).  G2, the fragmented 64-KiB
+payloads and equal-length ragged batches.
+    ENET_CRC_AMD_LIB=rusty_enet_amd/lib/variants/libenet_crc_amd_stamps.so python scripts/exp_round_stamps.py
 """
 import ctypes
 import os
@@ -19,8 +21,7 @@ import rusty_enet_amd as rea  # noqa: E402
 from rusty_enet_amd import _native  # noqa: E402
 from _data import ENET_SEED, packed_offsets, ragged_lengths  # noqa: E402
 
-L = _native.lib()
-f = L.enet_crc_debug_spin_stats
+f = _native.lib().enet_crc_debug_round_stamps
 f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 8)()
 dev = torch.device("cuda:0")
@@ -49,6 +50,8 @@ for name, lengths in cases.items():
     e1.synchronize()
     assert f(buf, 1) == 0
     us = e0.elapsed_time(e1) / reps * 1000
-    v = [x / reps for x in buf]
-    print(f"{name:22s} {us:8.1f} us/launch  polls per launch: ready {v[0]:9.0f} ({v[1]:7.0f} waits)  "
-          f"consumed {v[2]:9.0f} ({v[3]:7.0f})  freed {v[4]:9.0f} ({v[5]:7.0f})", flush=True)
+    body, loop, rounds, build, comb, make = buf[0], buf[1], buf[2], buf[3], buf[4], buf[5]
+    rest = loop - body - build - comb - make
+    print(f"{name:22s} {us:8.1f} us/launch  {rounds / reps:9.0f} rounds  per round (cycles): body "
+          f"{body / rounds:7.0f}, combine {comb / rounds:6.0f}, plan {make / rounds:6.0f}, builds "
+          f"{build / rounds:6.0f}, rest {rest / rounds:6.0f}  (body {100 * body / loop:4.1f} % of the loop)", flush=True)
