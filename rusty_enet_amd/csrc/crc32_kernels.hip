@@ -1207,126 +1207,10 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
 //     by ds_bpermute from lane (j2 - j1 + k) mod 8 of that group, and runs one more
 //     Horner step (the other lanes' last chunk was slot NSL - 1).
 // The launch covers count / 8 whole rounds; launch_uniform sends the < 8 packets left to
-// the register kernel.  Two forms: crc32_uniform_lines_kernel (the product) streams the
-// lines through a register ring like crc32_uniform_regs_kernel; crc32_uniform_lines_dma_kernel
-// (A/B builds only, -DENET_CRC_LINES_DMA) through the LDS-DMA ring of
-// crc32_uniform_dma_kernel.  Same lines, same lookups.
+// the register kernel.  The lines stream through a register ring like
+// crc32_uniform_regs_kernel's (the same lines through the LDS-DMA ring measured 3-5 % slower:
+// profiles/r03/parked/lines_dma_ring_kernel.patch).
 // ---------------------------------------------------------------------------------
-#ifndef ENET_CRC_LINES_AUX
-#define ENET_CRC_LINES_AUX 2  // non-temporal (an A/B build may set 0: default cache policy)
-#endif
-
-template <int NSL>
-__global__ __launch_bounds__(kBlock) void crc32_uniform_lines_dma_kernel(UniformBatch u, uint32_t* __restrict__ out) {
-  send_servers_home();
-  constexpr int R = kUniformRing;
-  static_assert(NSL >= R, "the ring reaches at most one round ahead");
-  __shared__ __attribute__((aligned(16))) UniformDmaLds<R> S;
-  uint32_t* const lds = S.tables;
-  auto& ring = S.ring;
-  constexpr int kLook = 2;
-  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kLook;
-  fill_lds(lds);
-  __syncthreads();
-  const LaneConsts c = lane_consts(u.base);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t rounds = u.count / kPacketsPerWave;  // whole rounds only (launch contract)
-  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
-  auto round_of = [&](uint32_t d) -> uint64_t {
-    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
-  };
-  const LinesLane ll = lines_lane(u.length, NSL, c.grp, c.k);
-  const uint64_t round_bytes = (uint64_t)kPacketsPerWave * u.length;
-  // This lane's slot-0 chunk in round rnd (rounds past the end re-read the last one).
-  auto lane_base = [&](uint64_t rnd) -> uint64_t {
-    return u.base + (rnd < rounds ? rnd : rounds - 1) * round_bytes + (uint64_t)ll.off0;
-  };
-  auto src_of = [&](uint64_t lb, int s) -> uint64_t {
-    return s == 0 && ll.dummy0 ? c.dummy : lb + (uint64_t)kBytesPerStep * (uint64_t)s;
-  };
-  const uint32_t ring0 = (uint32_t)(uintptr_t)(LdsVoid*)&ring[0][wv][0];
-  auto dma = [&](uint64_t src, uint32_t q) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)&ring[q][wv][0], 16, 0, ENET_CRC_LINES_AUX);
-  };
-
-  uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
-  if (rnd0 >= rounds) return;
-  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
-  {
-    const uint64_t lb = lane_base(rnd0);
-#pragma unroll
-    for (int f = 0; f < R; ++f) dma(src_of(lb, f), (uint32_t)f);
-  }
-  uint32_t q = 0;
-  u32x4 nextv = read_landed_slot<R - 1>(ring0 + lane * 16u);
-  uint32_t res = 0, j = 0;
-  uint64_t res_round = 0;
-  while (rnd0 < rounds) {
-    uint32_t d = 0;
-    if (lane == 0) d = lds_fetch_add_one(&S.next_dispatch);
-    const uint64_t lb = lane_base(rnd0), lbn = lane_base(rnd1);
-    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    u32x4 kept = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int s = 0; s < NSL; ++s) {
-      const u32x4 v = nextv;
-      const int f = s + R;  // refill this slot's LDS slot R slots ahead
-      dma(f < NSL ? src_of(lb, f) : src_of(lbn, f - NSL), q);
-      q = q + 1 == (uint32_t)R ? 0u : q + 1;
-      const uint32_t next_addr = ring0 + q * kRingStride + lane * 16u;
-      uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-      if (s < 2) {  // the group's first line: slot 0, or slot 1 after a zero slot 0
-        if (ll.keep[s]) kept = v;
-        w0 = (w0 & ll.am[s]) ^ ll.xm[s];
-        w1 &= ll.am[s];
-        w2 &= ll.am[s];
-        w3 &= ll.am[s];
-      }
-      if (s == 0) {  // h = 0 on every lane: M32^32(0) = 0, no lookups
-        h0 = w0;
-        h1 = w1;
-        h2 = w2;
-        h3 = w3;
-        nextv = read_landed_slot<R - 1>(next_addr);
-      } else {
-        horner_step_and_read<R - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, nextv);
-      }
-      issue_order_fence();
-    }
-    // Step 0 of the lanes whose last chunk lies in the next group's first line.
-    {
-      const uint32_t a = ll.src4;
-      const uint32_t x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.x);
-      const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.y);
-      const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.z);
-      const uint32_t x3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.w);
-      const uint32_t s0 = horner_main(lds, h0, x0, c.lk), s1 = horner_main(lds, h1, x1, c.lk);
-      const uint32_t s2 = horner_main(lds, h2, x2, c.lk), s3 = horner_main(lds, h3, x3, c.lk);
-      h0 = ll.lo ? s0 : h0;
-      h1 = ll.lo ? s1 : h1;
-      h2 = ll.lo ? s2 : h2;
-      h3 = ll.lo ? s3 : h3;
-    }
-    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-    const uint32_t reg = finish_word(lds, y, 0u, c.lk);  // lane k == 0 holds the register
-    const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
-    if (c.k == j) {
-      res = crc;
-      res_round = rnd0;
-    }
-    rnd0 = rnd1;
-    rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
-    if (j == 7u || rnd0 >= rounds) {
-      if (c.k <= j) out[res_round * kPacketsPerWave + c.grp] = res;
-      j = 0;
-    } else {
-      ++j;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // the ring's last DMAs land before the wave's LDS goes away
-}
-
 typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4;
 
 template <int NSL>
@@ -2052,10 +1936,6 @@ static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length) {
 
 template <int NSL>
 static hipError_t launch_uniform_lines(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
-#ifdef ENET_CRC_LINES_DMA  // A/B build: the same lines through the LDS-DMA ring
-  hipLaunchKernelGGL((crc32_uniform_lines_dma_kernel<NSL>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
-  return hipGetLastError();
-#endif
   hipLaunchKernelGGL((crc32_uniform_lines_kernel<NSL>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
