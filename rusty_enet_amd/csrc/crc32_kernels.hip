@@ -896,7 +896,8 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_dma_kernel(UniformBatch 
 }
 
 // ---------------------------------------------------------------------------------
-// Wave-per-packet kernel for long uniform packets (the default from 4 KiB): the whole wave
+// Wave-per-packet kernel for long uniform packets (from 4 KiB; packets of a multiple of 8 KiB
+// steps take the register-ring form crc32_wave_regs_kernel below): the whole wave
 // works on ONE packet and each step is one KiB of it, lane l taking the 16-B chunk
 // at a1 - 16 (l + 1) - 1024 (ns - 1 - s).  So every DMA instruction reads 1 KiB of
 // contiguous bytes (8 consecutive 128-B lines) instead of one line from each of 8
@@ -1049,6 +1050,107 @@ __global__ __launch_bounds__(kBlock) void crc32_wave_dma_kernel(UniformBatch u, 
     rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
   }
   __builtin_amdgcn_s_waitcnt(0);
+}
+
+// crc32_wave_dma_kernel with the slots in a register ring of kWaveRegRing KiB per wave
+// (non-temporal global loads when kNT) instead of the LDS-DMA ring, for packets of a multiple
+// of kWaveRegRing KiB steps (the 64-KiB buffers of configs[4]): 327-329 us vs 334-339 us for
+// 32,768 x 64 KiB, 4 alternating pairs (profiles/r03/waveregs).  Same arithmetic, masks,
+// dispatch and combine; the next packet's first kWaveRegRing steps load during the last ones.
+constexpr int kWaveRegRing = 8;
+typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4W;
+
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void crc32_wave_regs_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  send_servers_home();
+  constexpr int D = kWaveRegRing;
+  __shared__ __attribute__((aligned(16))) WaveDmaLds S;
+  uint32_t* const lds = S.tables;
+  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
+  fill_lds_wave(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(u.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t total = u.count;
+  const uint64_t sweep = (uint64_t)gridDim.x * kWavesPerBlock;
+  auto round_of = [&](uint32_t d) -> uint64_t {
+    return (uint64_t)blockIdx.x * kWavesPerBlock + (d % kWavesPerBlock) + (uint64_t)(d / kWavesPerBlock) * sweep;
+  };
+  const uint32_t lx = (u.length + 3u) & ~3u, z = lx - u.length;
+  const int32_t ns = (int32_t)((lx + kWaveStep - 1) / kWaveStep);  // a multiple of D (launch_uniform)
+  const uint32_t last_mask = lane == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+  const int64_t rel0 = (int64_t)lx - 16 * (int64_t)(lane + 1u) - (int64_t)kWaveStep * (ns - 1);
+  uint32_t am[4], xm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    am[j] = rel0 + 4 * j >= 0 ? 0xFFFFFFFFu : 0u;
+    xm[j] = rel0 + 4 * j == 0 ? kInitRegister : 0u;
+  }
+  const bool none0 = rel0 <= -16;
+  const bool part0 = rel0 < 0 && rel0 > -16;
+  const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;
+  auto packet_base = [&](uint64_t p) -> uint64_t { return u.base + (p < total ? p : total - 1) * u.stride; };
+  auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
+  auto slot_src = [&](uint64_t pb, int32_t s) -> uint64_t {
+    if (s != 0) return pb + (uint64_t)(rel0 + (int64_t)kWaveStep * s);
+    return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
+  };
+  auto ld = [&](uint64_t a) -> u32x4 {
+    if constexpr (kNT) return __builtin_nontemporal_load(reinterpret_cast<GlobalU32x4W*>(a));
+    return *reinterpret_cast<GlobalU32x4W*>(a);
+  };
+  uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
+  if (rnd0 >= total) return;
+  u32x4 q[D];
+  {
+    const uint64_t pb = packet_base(rnd0);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      q[i] = ld(slot_src(pb, i));
+      issue_order_fence();
+    }
+  }
+  const int32_t iters = ns / D;
+  while (rnd0 < total) {
+    uint32_t d = 0;
+    if (lane == 0) d = atomicAdd(&S.next_dispatch, 1u);
+    const uint64_t pb = packet_base(rnd0), pbn = packet_base(rnd1);
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    for (int32_t it = 0; it < iters; ++it) {
+      const bool first = it == 0, last = it == iters - 1;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        uint32_t w0 = q[i].x, w1 = q[i].y, w2 = q[i].z, w3 = q[i].w;
+        if (i == 0 && first) {
+          const bool below = is_below(pb);
+          if (__builtin_amdgcn_ballot_w64(below)) {
+            if (below) load_top_words(pb + (uint64_t)rel0, head_meta, c.dummy, w0, w1, w2, w3);
+          }
+        }
+        if (i == D - 1 && last) w3 &= last_mask;
+        if (i == 0 && first) {
+          h0 = (w0 & am[0]) ^ xm[0];
+          h1 = (w1 & am[1]) ^ xm[1];
+          h2 = (w2 & am[2]) ^ xm[2];
+          h3 = (w3 & am[3]) ^ xm[3];
+        } else {
+          h0 = horner_main(lds, h0, w0, c.lk);
+          h1 = horner_main(lds, h1, w1, c.lk);
+          h2 = horner_main(lds, h2, w2, c.lk);
+          h3 = horner_main(lds, h3, w3, c.lk);
+        }
+        issue_order_fence();
+        q[i] = ld(last ? slot_src(pbn, i) : slot_src(pb, (it + 1) * D + i));
+        issue_order_fence();
+      }
+    }
+    const uint32_t y = combine_wave(lds, h0, h1, h2, h3, c.lk);
+    const uint32_t reg = finish_word(lds, y, z, c.lk);
+    if (lane == 0) out[rnd0] = __builtin_bswap32(~reg);
+    rnd0 = rnd1;
+    rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1971,6 +2073,13 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
       uint64_t wblocks = (count + kWavesPerBlock - 1) / kWavesPerBlock;
       const int cus = cu_count_for_current_device();
       if (wblocks > (uint64_t)cus) wblocks = (uint64_t)cus;
+      if ((((length + 3u) & ~3u) + kWaveStep - 1) / kWaveStep % kWaveRegRing == 0) {
+        if (nt_lines(u))
+          hipLaunchKernelGGL((crc32_wave_regs_kernel<true>), dim3((unsigned)wblocks), dim3(kBlock), 0, stream, u, out);
+        else
+          hipLaunchKernelGGL((crc32_wave_regs_kernel<false>), dim3((unsigned)wblocks), dim3(kBlock), 0, stream, u, out);
+        return hipGetLastError();
+      }
       if (nt_lines(u))
         hipLaunchKernelGGL((crc32_wave_dma_kernel<true>), dim3((unsigned)wblocks), dim3(kBlock), 0, stream, u, out);
       else

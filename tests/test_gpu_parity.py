@@ -327,9 +327,11 @@ def test_long_packets_wave_kernel(dev, base_off):
     # Lengths from the 4-KiB minimum up, multiples of 1 KiB and 128 B or not, odd lengths
     # (bytes past the end masked), gaps between packets, packets within a chunk of the
     # base (fallback loads), counts that are not multiples of the wave count.
+    # Packets of a multiple of 8 KiB steps take the register-ring form (crc32_wave_regs_kernel),
+    # the others the LDS-DMA ring.
     for stride, length, n in [(65536, 65536, 200), (4096, 4096, 3001), (4100, 4097, 999), (5000, 4999, 777),
                               (12288, 10001, 300), (65540, 65537, 33), (70000, 65536, 17), (8192, 8191, 1),
-                              (4096, 4096, 4097)]:
+                              (4096, 4096, 4097), (32768, 32768, 501), (24580, 24573, 333), (16384, 16381, 1025)]:
         data = splitmix64_bytes(base_off * 3 + stride + length, base_off + (n - 1) * stride + length)
         d = to_dev(data, dev)[base_off:]
         got = as_u32(rea.crc32_batch(d, stride=stride, length=length, count=n))
