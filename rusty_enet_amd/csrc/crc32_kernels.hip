@@ -306,25 +306,26 @@ __device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32
   return y;
 }
 
-// The ragged jobs kernel's tables: fill_lds's, plus M32^2 and M32^12 (kJobsM2Dword).
+// The ragged jobs kernel's tables: fill_lds's, plus M32^12 (kJobsM12Dword).
 __device__ __forceinline__ void fill_lds_jobs(uint32_t* lds) {
   fill_lds(lds);
   for (int x = threadIdx.x; x < 1024; x += kBlock) {
-    lds[kJobsM2Dword + x] = g_op_tables.op[1][x >> 8][x & 255];
     lds[kJobsM12Dword + x] = g_op_tables.m12[x >> 8][x & 255];
   }
 }
 
-// combine_tree in 4 dependent LDS round trips instead of 6 (the ragged jobs kernel, whose
-// per-round overhead is mostly such round trips): in-lane a = M h0 ^ h1 and b = M h2 ^ h3
-// side by side, then y = M^2 a ^ b; across the group a radix-4 tree: lane k = 4i + q applies
-// M^(4q) (q = 1, 2, 3: M^4, M^8, M^12), lanes 4i gather their quad by DPP, lane 4 applies
-// M^16 and lane 0 adds it.  The result equals combine_tree's: sum over k of M^(4k) y_k.
+// combine_tree with a radix-4 tree across the group (the ragged jobs kernel, whose per-round
+// overhead is mostly dependent LDS round trips): the in-lane Horner (3 conflict-free trips),
+// then lane k = 4i + q applies M^(4q) (q = 1, 2, 3: M^4, M^8, M^12), lanes 4i gather their
+// quad by DPP, lane 4 applies M^16 and lane 0 adds it: 5 trips instead of 6.  (The in-lane
+// part in two trips through an unreplicated M32^2 doubled the kernel's bank conflicts and was
+// 1.5 % slower: profiles/r03/inlane.)  The result equals combine_tree's: sum over k of
+// M^(4k) y_k.
 __device__ __forceinline__ uint32_t combine_tree_jobs(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
                                                      uint32_t h3, const Lookup& lk) {
-  const uint32_t a = apply_rep(lds, h0, h1, lk.lp1, lk);
-  const uint32_t b = apply_rep(lds, h2, h3, lk.lp1, lk);
-  uint32_t y = apply_small(lds + kJobsM2Dword, a) ^ b;
+  uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
+  y = apply_rep(lds, y, h2, lk.lp1, lk);
+  y = apply_rep(lds, y, h3, lk.lp1, lk);
   const uint32_t k = threadIdx.x & (G - 1), q = k & 3u;
   uint32_t t = y;
   if (q != 0) {
