@@ -306,38 +306,6 @@ __device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32
   return y;
 }
 
-// The ragged jobs kernel's tables: fill_lds's, plus M32^12 (kJobsM12Dword).
-__device__ __forceinline__ void fill_lds_jobs(uint32_t* lds) {
-  fill_lds(lds);
-  for (int x = threadIdx.x; x < 1024; x += kBlock) {
-    lds[kJobsM12Dword + x] = g_op_tables.m12[x >> 8][x & 255];
-  }
-}
-
-// combine_tree with a radix-4 tree across the group (the ragged jobs kernel, whose per-round
-// overhead is mostly dependent LDS round trips): the in-lane Horner (3 conflict-free trips),
-// then lane k = 4i + q applies M^(4q) (q = 1, 2, 3: M^4, M^8, M^12), lanes 4i gather their
-// quad by DPP, lane 4 applies M^16 and lane 0 adds it: 5 trips instead of 6.  (The in-lane
-// part in two trips through an unreplicated M32^2 doubled the kernel's bank conflicts and was
-// 1.5 % slower: profiles/r03/inlane.)  The result equals combine_tree's: sum over k of
-// M^(4k) y_k.
-__device__ __forceinline__ uint32_t combine_tree_jobs(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
-                                                     uint32_t h3, const Lookup& lk) {
-  uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
-  y = apply_rep(lds, y, h2, lk.lp1, lk);
-  y = apply_rep(lds, y, h3, lk.lp1, lk);
-  const uint32_t k = threadIdx.x & (G - 1), q = k & 3u;
-  uint32_t t = y;
-  if (q != 0) {
-    const uint32_t set = q == 1 ? kTreeDword : (q == 2 ? kTreeDword + 1024 : kJobsM12Dword);
-    t = apply_small(lds + set, y);
-  }
-  y = t ^ from_lane_plus<1>(t) ^ from_lane_plus<2>(t) ^ from_lane_plus<3>(t);  // valid on lanes 4i
-  uint32_t u = 0;
-  if (k == 4u) u = apply_small(lds + kTreeDword + 2048, y);  // M32^16
-  return y ^ from_lane_plus<4>(u);
-}
-
 __device__ __forceinline__ void fill_lds_regs(uint32_t* lds) {
   fill_replicated(lds, kMainLevel);
   fill_replicated(lds + kTreeRepDword, 2, 3);
@@ -1625,7 +1593,7 @@ struct JobSlot {
   uint32_t res[kJobPackets];
 };
 struct RaggedJobsLds {
-  uint32_t tables[kJobsLdsDwords];
+  uint32_t tables[kLdsDwords];
   u32x4 ring[kRaggedRing][kWavesPerBlock][64];
   JobSlot job[kJobSlots];
   uint32_t ready[kJobSlots];     // k + 1 once the workgroup's k-th job has its records here
@@ -1705,7 +1673,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     S.freed[threadIdx.x] = 0;
   }
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kLook;
-  fill_lds_jobs(lds);
+  fill_lds(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1894,7 +1862,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     st_body += st_b1 - st_b0;
     ++st_rounds;
 #endif
-    const uint32_t y = combine_tree_jobs(lds, h0, h1, h2, h3, c.lk);
+    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
 #ifdef ENET_CRC_ROUND_STAMPS

@@ -37,10 +37,6 @@ constexpr uint32_t kLdsDwords = kTreeDword + kTreeLevels * 1024;
 constexpr uint32_t kTreeRepDword = kRepDwords;
 constexpr uint32_t kTree16Dword = 2 * kRepDwords;
 constexpr uint32_t kRegsLdsDwords = kTree16Dword + 1024;
-// Layout of the ragged jobs kernel: the unreplicated tree sets M32^4, M32^8, M32^16 of
-// kLdsDwords, then M32^12 (its radix-4 tree).
-constexpr uint32_t kJobsM12Dword = kTreeDword + kTreeLevels * 1024;
-constexpr uint32_t kJobsLdsDwords = kJobsM12Dword + 1024;
 static_assert(kMainLevel < kOpLevels, "operator level");
 static_assert(kRepCopies * 4 == 32, "8 copies x 4 tables cover the 32 banks of a ds_read_b32 lane group");
 

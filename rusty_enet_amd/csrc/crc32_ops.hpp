@@ -33,7 +33,6 @@ constexpr int kOpLevels = 9;  // M32^1 .. M32^256
 struct OpTables {
   uint32_t sarwate[256];
   uint32_t op[kOpLevels][4][256];
-  uint32_t m12[4][256];  // M32^12 = M32^8 o M32^4 (the ragged kernel's radix-4 combine tree)
   uint32_t head_k[4];
   uint8_t inv_top[256];  // inv_top[sarwate[b] >> 24] = b (see m8_inverse)
 };
@@ -78,9 +77,6 @@ constexpr OpTables make_op_tables() {
         t.op[lv][k][b] = x;
       }
     }
-  }
-  for (int k = 0; k < 4; ++k) {
-    for (uint32_t b = 0; b < 256; ++b) t.m12[k][b] = apply_op(t.op[3], apply_op(t.op[2], b << (8 * k)));
   }
   for (uint32_t b = 0; b < 256; ++b) t.inv_top[t.sarwate[b] >> 24] = (uint8_t)b;
   uint32_t k = kInitRegister;
