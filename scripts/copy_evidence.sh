@@ -1,0 +1,17 @@
+#!/usr/bin/env bash
+# Copy one gpu_r03_final.sh / gpu_profile_round.sh run into a profiles/ directory and
+# profiles/pmc_traffic.json (bench.py reads the traffic only while the kernel-source hash
+# inside still matches the sources).
+#   bash scripts/copy_evidence.sh gpurun_out/<tag> profiles/<round>/final
+set -eu
+SRC="$1"; DST="$2"
+mkdir -p "$DST"
+for c in uniform ragged large range; do
+  cp "$SRC/bench_$c.json" "$DST/"
+  cp "$SRC/prof_$c/run_kernel_stats.csv" "$DST/${c}_kernel_stats.csv"
+  python3 scripts/pmc_summary.py "$SRC/pmc_$c" > "$DST/${c}_pmc_summary.txt" 2>&1
+done
+for f in ipc_uniform_summary.txt ipc_ragged_summary.txt traffic.json pytest_gpu.log bench_rehearsal_n2.json; do
+  [ -f "$SRC/$f" ] && cp "$SRC/$f" "$DST/"
+done
+cp "$SRC/traffic.json" profiles/pmc_traffic.json
