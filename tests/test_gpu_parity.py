@@ -152,6 +152,26 @@ def test_full_size_ragged_1m(dev):
     assert np.array_equal(got, _oracle.crc32_ragged(d.cpu().numpy(), offsets, lengths))
 
 
+def test_kernels_agree_on_the_same_bytes(dev):
+    """HIP against HIP: the same packets through the uniform kernels (stride form) and the
+    ragged jobs kernel (offsets / lengths form) give the same checksums, for G1's 1200-B
+    packets (whole-line kernel), 1393-B packets at an odd stride (register ring) and 64-KiB
+    buffers (wave-per-packet kernel); a sample is also checked against the oracle."""
+    for n, stride, L, seed in ((1 << 18, 1200, 1200, 91), (1 << 16, 1396, 1393, 92), (512, 65536, 65536, 93)):
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        d = torch.randint(0, 256, ((n - 1) * stride + L,), dtype=torch.uint8, device=dev, generator=g)
+        uni = as_u32(rea.crc32_batch(d, stride=stride, length=L, count=n))
+        offsets = np.arange(n, dtype=np.int64) * stride
+        rag = as_u32(rea.crc32_batch(d, offsets=to_dev(offsets, dev),
+                                     lengths=to_dev(np.full(n, L, dtype=np.int32), dev)))
+        assert np.array_equal(uni, rag), (stride, L)
+        host = d.cpu().numpy()
+        k = min(n, 512)
+        want = _oracle.crc32_uniform(host[:(k - 1) * stride + L], stride, L, k, threads=8)
+        assert np.array_equal(uni[:k], want), (stride, L)
+
+
 def test_full_shard_uniform_2m_x_1200(dev):
     """The per-GPU shard of configs[3] (16M x 1200 B over 8 GPUs): 2M x 1200 B = 2.4 GB."""
     n, L = 2 << 20, 1200
