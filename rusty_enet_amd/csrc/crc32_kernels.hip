@@ -1403,6 +1403,9 @@ struct RaggedRound {
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
   bool direct;          // top chunk read directly (not fallback / not before the packet)
   bool fast;            // wave-uniform: every lane's top is the same slot, no fallback, ns <= kRaggedFastMax
+  bool live;            // jobs kernel: the round is inside the batch (wave-uniform)
+  uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
+  uint32_t job_rounds;  // jobs kernel: rounds of that job
   int32_t top_uniform;  // that slot (0 unless ns == kRaggedRing and the packets are shorter)
 };
 
@@ -1690,9 +1693,15 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   // per job (only the batch's last job has fewer).  Monotone: once a round is past the
   // batch, so is every later one.
   const uint32_t RJ = JP / kPacketsPerWave;
+  // d / RJ as one s_mul_hi: M = ceil(2^32 / RJ) is exact for d < 2^27 rounds (RJ <= 32;
+  // launch_ragged keeps the rounds of a workgroup far below that).  hipcc's expansion of
+  // the division is 11 scalar instructions, and this loop is issue-bound.
+  const uint32_t rj_magic = 0xFFFFFFFFu / RJ + 1u;
+  auto div_rj = [&](uint32_t x) -> uint32_t { return __umulhi(x, rj_magic); };
   auto round_valid = [&](uint32_t d) -> bool {
-    const uint64_t J = job_of(d / RJ);
-    return J < b.njobs && (uint64_t)(d % RJ) * kPacketsPerWave < job_count(J);
+    const uint32_t k = div_rj(d);
+    const uint64_t J = job_of(k);
+    return J < b.njobs && (uint64_t)(d - k * RJ) * kPacketsPerWave < job_count(J);
   };
 
   // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
@@ -1795,21 +1804,28 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   auto make_round = [&](uint32_t d) -> RaggedRound {
     uint64_t ax = 0;
     uint32_t info = 0;
-    const uint32_t k = d / RJ, slot = k % kJobSlots;
-    bool rv = round_valid(d);
+    const uint32_t k = div_rj(d), slot = k % kJobSlots;
+    const uint64_t J = job_of(k);
+    const uint32_t n = J < b.njobs ? job_count(J) : 0u;
+    const bool live = (d - k * RJ) * kPacketsPerWave < n;  // round_valid(d)
+    bool rv = live;
     if (rv && k + 1u > seen_ready) {
       rv = lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u);
       if (rv) seen_ready = k + 1u;
     }
     if (rv) {
-      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d % RJ) * kJobRoundBytes;
+      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
       asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"  // one round trip
                    : "=&v"(ax), "=&v"(info)
                    : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp)
                    : "memory");
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
     }
-    return round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
+    RaggedRound rr = round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
+    rr.live = live;
+    rr.job_k = k;
+    rr.job_rounds = (n + kPacketsPerWave - 1) / kPacketsPerWave;
+    return rr;
   };
 
   uint32_t rnd0 = wv, rnd1 = wv + kWavesPerBlock;
@@ -1828,7 +1844,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   uint64_t st_body = 0, st_build = 0, st_rounds = 0, st_comb = 0, st_make = 0;
   const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
 #endif
-  while (round_valid(rnd0)) {
+  while (cur.live) {  // cur is round rnd0
     uint32_t d = 0;
     if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
     d = __builtin_amdgcn_readfirstlane(d);
@@ -1838,8 +1854,8 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     // the iteration that claimed it, and nothing there waits for a younger job (the
     // checksum slot below waits only for an older job's flush).
     bool build = false;
-    const uint32_t kb = d / RJ + kJobAhead, bslot = kb % kJobSlots;
-    if (d % RJ == 0 && kb >= first_jobs && job_of(kb) < b.njobs) {
+    const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
+    if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
       build = kb < (uint32_t)kJobSlots || lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ);
       if (build) {
         if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
@@ -1871,7 +1887,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
 #endif
     // The round's checksums into the job's result array; the last round of a job
     // writes the job's checksums to HBM.
-    const uint32_t k0 = rnd0 / RJ, slot0 = k0 % kJobSlots;
+    const uint32_t k0 = cur.job_k, slot0 = k0 % kJobSlots;
     if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
       if (lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
@@ -1882,9 +1898,9 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
     old = __builtin_amdgcn_readfirstlane(old);
-    const uint64_t J0 = job_of(k0);
-    const uint32_t n0 = job_count(J0);
-    if (old + 1u == (n0 + kPacketsPerWave - 1) / kPacketsPerWave) {
+    if (old + 1u == cur.job_rounds) {
+      const uint64_t J0 = job_of(k0);
+      const uint32_t n0 = job_count(J0);
       const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
       uint32_t* dst = out + J0 * JP + 4u * lane;
       if (4u * lane + 4u <= n0) {
