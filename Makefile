@@ -16,7 +16,14 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++20 -fPIC -fvisibility=hidden -Wal
 # tests/test_gpu_hooks.py through ENET_CRC_AMD_LIB, never by the product.
 TESTLIB := rusty_enet_amd/lib/variants/libenet_crc_amd_testhooks.so
 
-all: $(LIB) $(TESTLIB) $(ORACLE) $(ORACLE_RANGE)
+# Same-process HBM read ceiling (bench.py's roofline.read_ceiling_gbs; tooling, not product).
+CEILING := tools/lib/libenet_read_ceiling.so
+
+all: $(LIB) $(TESTLIB) $(ORACLE) $(ORACLE_RANGE) $(CEILING)
+
+$(CEILING): tools/ceiling/read_ceiling.hip
+	mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 $(LIB): $(HIP_DEP)
 	mkdir -p $(dir $@)
@@ -30,7 +37,7 @@ $(ORACLE): oracle/crc32_oracle.c
 	$(CC) -O2 -fPIC -shared -pthread -Wall -o $@ $<
 
 clean:
-	rm -f $(LIB) $(TESTLIB) $(ORACLE) $(ORACLE_RANGE)
+	rm -f $(LIB) $(TESTLIB) $(ORACLE) $(ORACLE_RANGE) $(CEILING)
 
 .PHONY: all clean
 
@@ -38,7 +45,7 @@ $(ORACLE_RANGE): oracle/range_coder_oracle.c
 	$(CC) -O2 -fPIC -shared -Wall -o $@ $<
 
 # A/B builds of the library with compile-time variant switches (never the product):
-#   make variant NAME=region DEFS=-DENET_CRC_REGION_RAGGED
+#   make variant NAME=nolines DEFS=-DENET_CRC_NO_LINES
 #   -> rusty_enet_amd/lib/variants/libenet_crc_amd_region.so, loaded with ENET_CRC_AMD_LIB.
 variant: $(HIP_DEP)
 	mkdir -p rusty_enet_amd/lib/variants

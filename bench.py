@@ -355,7 +355,7 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
             ctx.crc32(pkt)
         variants[name] = round((time.perf_counter() - t0) / calls * 1e6, 2)
     ctx.set_percall_mode(_native.ENET_CRC_PERCALL_ZEROCOPY)  # stops the server wave
-    per_call_us = variants["persistent"]  # the context's default mode
+    per_call_us = variants["zerocopy"]  # the context's default mode (ENET_CRC_PERCALL_ZEROCOPY, ABI >= 5)
     # Floor of any per-call GPU path: one trivial kernel launch + stream synchronize.
     import torch
 
@@ -381,7 +381,8 @@ def end_to_end(dev, n: int = 1 << 18, L: int = 1200) -> dict:
             "per_call_cpu_oracle_us": round(cpu_call_us, 2),
             "per_call_floor_us": round(floor_us, 2),
             "per_call_sample": "enet_crc32_iov on one 1392-B datagram (the HostSettings::checksum hook), mean of 2000, "
-                               "default mode (persistent server wave; variants: copy, zero-copy launch, persistent); "
+                               "default mode (zero-copy launch; variants: copy, zero-copy launch, opt-in persistent "
+                               "server wave); "
                                "cpu: the C restatement of src/crc32.rs on the same datagram through ctypes; floor: one "
                                "trivial torch kernel launch + torch.cuda.synchronize",
             "ring": ring_rate(dev, L)}
@@ -423,6 +424,100 @@ def ring_rate(dev, L: int = 1200, nslots: int = 4, per_slot: int = 40000, rounds
 # --------------------------------------------------------------------------------------
 # roofline evidence
 # --------------------------------------------------------------------------------------
+
+CEILING_LIB = os.path.join(REPO, "tools", "lib", "libenet_read_ceiling.so")
+
+
+class ReadCeiling:
+    """tools/ceiling/read_ceiling.hip: a pure streaming read (16-B loads, XOR only) of the
+    same device buffer the bench checksums, launched on torch's current stream.  Its best
+    variant's rate is the same-process ceiling the kernel is stated against
+    (roofline.read_ceiling_gbs / frac_of_ceiling).  Measurement tooling:
+    never on the product path."""
+
+    def __init__(self, dev):
+        import ctypes
+
+        import torch
+
+        if not os.path.exists(CEILING_LIB):
+            raise FileNotFoundError(f"{CEILING_LIB} not built (make all)")
+        self._lib = ctypes.CDLL(CEILING_LIB)
+        self._lib.enet_read_ceiling.restype = ctypes.c_int
+        self._lib.enet_read_ceiling.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                ctypes.c_void_p]
+        self._lib.enet_read_ceiling_name.restype = ctypes.c_char_p
+        self._lib.enet_read_ceiling_name.argtypes = [ctypes.c_int]
+        self._lib.enet_read_ceiling_bytes.restype = ctypes.c_uint64
+        self._lib.enet_read_ceiling_bytes.argtypes = [ctypes.c_uint64]
+        self.variants = int(self._lib.enet_read_ceiling_variants())
+        self.dev = dev
+        self._out = torch.zeros(4, dtype=torch.int32, device=dev)
+
+    def name(self, v: int) -> str:
+        return self._lib.enet_read_ceiling_name(v).decode()
+
+    def bytes_read(self, nbytes: int) -> int:
+        return int(self._lib.enet_read_ceiling_bytes(nbytes))
+
+    def launch(self, v: int, data, nbytes: int) -> None:
+        import torch
+
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        st = self._lib.enet_read_ceiling(v, data.data_ptr(), nbytes, self._out.data_ptr(), stream)
+        if st != 0:
+            raise RuntimeError(f"enet_read_ceiling({v}): hipError {st}")
+
+    def measure(self, data, nbytes: int, launches: int = 10, variants=None) -> dict:
+        """Each variant (default: all): one untimed launch, then `launches` timed back to back
+        (HIP events on the launch stream).  Returns the best rate and each variant's."""
+        import torch
+
+        stream = torch.cuda.current_stream(self.dev)
+        nread = self.bytes_read(nbytes)
+        per, index = {}, {}
+        for v in (range(self.variants) if variants is None else variants):
+            self.launch(v, data, nbytes)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(stream)
+            for _ in range(launches):
+                self.launch(v, data, nbytes)
+            ev1.record(stream)
+            torch.cuda.synchronize()
+            us = ev0.elapsed_time(ev1) * 1000.0 / launches
+            per[self.name(v)] = {"us": round(us, 2), "gbs": round(nread / us / 1e3, 1)}
+            index[self.name(v)] = v
+        best = max(per, key=lambda k: per[k]["gbs"])
+        return {"gbs": per[best]["gbs"], "variant": best, "variant_index": index[best], "bytes": nread,
+                "launches": launches, "variants": per}
+
+
+def open_ceiling(dev):
+    """ReadCeiling on `dev`, or None when the tooling library is not built (the line then
+    says so instead of failing)."""
+    try:
+        return ReadCeiling(dev)
+    except (OSError, FileNotFoundError):
+        return None
+
+
+def ceiling_fields(ceil, pre: dict | None, data, nbytes: int, achieved_gbs: float) -> dict:
+    """The same-buffer read ceiling around a timed region: `pre` was measured (all variants)
+    just before the warmup steps, this measures the best variant again right after the timed
+    steps; frac_of_ceiling = the kernel's algorithmic GB/s / that rate."""
+    if ceil is None or pre is None:
+        return {"read_ceiling_gbs": None, "frac_of_ceiling": None,
+                "read_ceiling": {"note": f"{CEILING_LIB} not built"}}
+    post = ceil.measure(data, nbytes, launches=20, variants=[pre["variant_index"]])
+    return {"read_ceiling_gbs": post["gbs"], "frac_of_ceiling": round(achieved_gbs / post["gbs"], 4),
+            "read_ceiling": {"after_gbs": post["gbs"], "before_gbs": pre["gbs"], "variant": pre["variant"],
+                             "bytes": post["bytes"], "before_variants": pre["variants"],
+                             "what": "tools/ceiling/read_ceiling.hip: the same device buffer read once with 16-B "
+                                     "loads and an XOR, best of its variants measured before the warmup steps "
+                                     "(which also takes the GPU through its power-management transient, "
+                                     "DESIGN.md §6) and that variant again right after the timed steps "
+                                     "(after_gbs = read_ceiling_gbs, 20 launches)"}}
+
 
 def kernel_source_hash() -> str:
     h = hashlib.sha256()
@@ -553,6 +648,8 @@ def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, bar
     step()
     torch.cuda.synchronize()
     verify_sample(out, spec)
+    ceil = open_ceiling(dev)
+    pre = ceil.measure(spec[1], nbytes) if ceil else None
     for _ in range(warmup):
         step()
     wall, kms = time_steps(step, steps, barrier, dev)
@@ -560,6 +657,8 @@ def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, bar
     res = {"packets": npk, "bytes": nbytes, "ms_per_step": round(ms, 5),
            "value": round(nbytes / (ms / 1000.0) / 2**30, 2), "unit": "GiB/s",
            "kernel_ms": round(kms, 5), "frac": round(nbytes / (kms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
+    cf = ceiling_fields(ceil, pre, spec[1] if ceil else None, nbytes, nbytes / (kms / 1000.0) / 1e9)
+    res["read_ceiling_gbs"], res["frac_of_ceiling"] = cf["read_ceiling_gbs"], cf["frac_of_ceiling"]
     del spec, out
     torch.cuda.empty_cache()
     return res
@@ -621,9 +720,15 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     if not args.no_verify:
         verify_sample(out, spec)
+    # Same-buffer read ceiling, all variants, before the warmup steps (range: not bound by
+    # streaming reads, no ceiling).
+    ceil = None if is_range else open_ceiling(dev)
+    ceil_pre = ceil.measure(spec[1], nbytes) if ceil else None
     for _ in range(args.warmup):
         step()
     wall, kernel_ms = time_steps(step, args.steps, barrier, dev)
+    ceil_fields = None if is_range else ceiling_fields(ceil, ceil_pre, spec[1] if ceil else None, nbytes,
+                                                      nbytes / (kernel_ms / 1000.0) / 1e9)
 
     from rusty_enet_amd.shards import max_over_ranks
 
@@ -674,6 +779,8 @@ def main(argv=None) -> int:
                          "traffic_source": traffic_src, "kernel_source_hash": kernel_source_hash(),
                          "kernel_ms": round(kernel_ms, 5), "kernel_ms_max_rank": round(kernel_ms_max, 5)},
         }
+        if ceil_fields:
+            line["roofline"].update(ceil_fields)
         line.update(extra)
         line["devices"] = devices
         if is_range:

@@ -53,6 +53,10 @@ extern "C" {
     pub fn enet_crc_strerror(status: c_int) -> *const core::ffi::c_char;
     pub fn enet_crc_last_hip_error() -> c_int;
     pub fn enet_crc_device_count() -> c_int;
+    /// Device-side failure channel (ABI 6): > 0 if a batch kernel on `device` gave up since
+    /// the last clear (its outputs are invalid); the synchronous entries return
+    /// ENET_CRC_E_DEVICE (-5) instead.
+    pub fn enet_crc_device_status(device: c_int, clear: c_int) -> c_int;
     pub fn enet_crc_ctx_create(device: c_int, out_ctx: *mut *mut enet_crc_ctx) -> c_int;
     pub fn enet_crc_ctx_create_multi(devices: *const c_int, ndevices: u32, out_ctx: *mut *mut enet_crc_ctx) -> c_int;
     pub fn enet_crc_ctx_destroy(ctx: *mut enet_crc_ctx);

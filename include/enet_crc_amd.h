@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ENET_CRC_ABI_VERSION 5
+#define ENET_CRC_ABI_VERSION 6
 
 #if defined(__GNUC__)
 #define ENET_CRC_API __attribute__((visibility("default")))
@@ -49,6 +49,9 @@ extern "C" {
 #define ENET_CRC_E_NO_DEVICE (-2) /* no HIP device / bad device index */
 #define ENET_CRC_E_HIP (-3)       /* a HIP runtime call failed; see enet_crc_last_hip_error() */
 #define ENET_CRC_E_NOMEM (-4)     /* host or device allocation failed */
+/* A batch kernel gave up on the device (an inter-wave wait of the ragged kernel timed out):
+ * the batch's outputs are invalid.  See enet_crc_device_status(). */
+#define ENET_CRC_E_DEVICE (-5)
 
 /* Shape of ENetBuffer {data, data_length} (src/c.rs:25-28): one input slice. */
 typedef struct enet_crc_iov {
@@ -92,14 +95,31 @@ typedef struct enet_crc_ctx enet_crc_ctx;
 #define ENET_CRC_PERCALL_PERSISTENT 2
 
 /* ENET_CRC_ABI_VERSION: 4 added enet_crc32_combine; 5 added enet_crc_ctx_percall_mode and
- * enet_crc_ctx_stop_server and made ZEROCOPY the default per-call mode.  Nothing was
- * removed. */
+ * enet_crc_ctx_stop_server and made ZEROCOPY the default per-call mode; 6 added
+ * ENET_CRC_E_DEVICE and enet_crc_device_status.  Nothing was removed. */
 ENET_CRC_API int enet_crc_abi_version(void);
 ENET_CRC_API const char* enet_crc_strerror(int status);
 /* hipError_t of the last failing HIP call made by this thread (0 if none). */
 ENET_CRC_API int enet_crc_last_hip_error(void);
 /* Number of visible HIP devices (0 when none), or a negative status. */
 ENET_CRC_API int enet_crc_device_count(void);
+
+/*
+ * Device-side failure channel.  The ragged batch kernel synchronises its waves through
+ * flags in LDS; a wait that does not complete within its poll limit (never observed:
+ * DESIGN.md §4) is given up rather than left to hang the GPU.  The wave that gives up
+ * writes a failure bit (1: a job's records never became ready, 2: a job slot was never
+ * released, 4: a result slot was never flushed) into the device's failure word, and its
+ * workgroup stops writing checksums.  The word is per device and sticky:
+ *   - the synchronous entries (enet_crc32_ragged_host, enet_crc_ring_wait, and the
+ *     receive/send loops built on them) check it after their last wait; if it is set they
+ *     clear it and return ENET_CRC_E_DEVICE: no output of that call may be trusted;
+ *   - after the asynchronous *_device entries, synchronise the stream and call
+ *     enet_crc_device_status(device, clear): > 0 means some batch on that device since
+ *     the last clear produced invalid outputs.
+ * Returns the bits (0 = no failure), or a negative status for a bad device.
+ */
+ENET_CRC_API int enet_crc_device_status(int device, int clear);
 
 /* Create a context bound to HIP device `device` (its own non-blocking streams,
  * pinned + device staging grown on demand).  Same as
@@ -170,7 +190,10 @@ ENET_CRC_API int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_
  * (d_offsets == NULL: packets at d_base + p*stride, `length` bytes) or ragged
  * (d_offsets/d_lengths) batch in device `device`'s memory, checksummed on that
  * device into d_out on hip_stream (a stream of that device, or NULL).  Every
- * launch is asynchronous; the shards run concurrently on their devices.
+ * launch is asynchronous (nothing waits: synchronise each shard's stream); the shards
+ * run concurrently on their devices.  Placement is checked before anything launches:
+ * d_base, d_out, d_offsets and d_lengths must be device memory of `device` and
+ * hip_stream a stream of `device`, else ENET_CRC_E_INVALID and no shard runs.
  */
 typedef struct enet_crc_shard {
   int device;

@@ -77,9 +77,12 @@ void oracle_crc32_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
   for (uint64_t i = 0; i < count; ++i) out[i] = oracle_crc32(base + i * stride, length);
 }
 
-/* Multi-threaded driver for the all-cores CPU baseline (packet range split). */
+/* Multi-threaded drivers (packet range split): the all-cores CPU baseline, and the
+ * checker for full-size GPU batches.  offsets == NULL: uniform packets at i * stride. */
 typedef struct {
   const uint8_t* base;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
   uint64_t stride;
   uint32_t length;
   uint64_t first, last;
@@ -88,28 +91,47 @@ typedef struct {
 
 static void* mt_worker(void* arg) {
   mt_job* j = (mt_job*)arg;
-  for (uint64_t i = j->first; i < j->last; ++i) j->out[i] = oracle_crc32(j->base + i * j->stride, j->length);
+  for (uint64_t i = j->first; i < j->last; ++i)
+    j->out[i] = j->offsets ? oracle_crc32(j->base + j->offsets[i], j->lengths[i])
+                           : oracle_crc32(j->base + i * j->stride, j->length);
   return NULL;
 }
 
-int oracle_crc32_uniform_mt(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
-                            uint32_t* out, int threads) {
+static int run_mt(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, uint64_t stride,
+                  uint32_t length, uint64_t count, uint32_t* out, int threads) {
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   pthread_t tid[256];
   mt_job jobs[256];
   pthread_once(&g_once, build_table);
+  int started = 0, rc = 0;
   for (int t = 0; t < threads; ++t) {
     jobs[t].base = base;
+    jobs[t].offsets = offsets;
+    jobs[t].lengths = lengths;
     jobs[t].stride = stride;
     jobs[t].length = length;
     jobs[t].first = count * (uint64_t)t / (uint64_t)threads;
     jobs[t].last = count * (uint64_t)(t + 1) / (uint64_t)threads;
     jobs[t].out = out;
-    if (pthread_create(&tid[t], NULL, mt_worker, &jobs[t]) != 0) return -1;
+    if (pthread_create(&tid[t], NULL, mt_worker, &jobs[t]) != 0) {
+      rc = -1;
+      break;
+    }
+    ++started;
   }
-  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
-  return 0;
+  for (int t = 0; t < started; ++t) pthread_join(tid[t], NULL);
+  return rc;
+}
+
+int oracle_crc32_uniform_mt(const uint8_t* base, uint64_t stride, uint32_t length, uint64_t count,
+                            uint32_t* out, int threads) {
+  return run_mt(base, NULL, NULL, stride, length, count, out, threads);
+}
+
+int oracle_crc32_ragged_mt(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, uint64_t count,
+                           uint32_t* out, int threads) {
+  return run_mt(base, offsets, lengths, 0, 0, count, out, threads);
 }
 
 /*

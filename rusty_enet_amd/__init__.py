@@ -15,6 +15,7 @@ from .checksum import (  # noqa: F401
     crc32_shards_device,
     crc32_uniform_device,
     default_context,
+    device_status,
     insert_batch,
     shard_bounds_native,
     slot_adjust,
@@ -25,6 +26,6 @@ from .range_coder import RangeCoder, compress_batch, decompress_batch, gather_sl
 
 __all__ = [
     "Context", "CrcError", "NativeLibraryMissing", "checksum_fn", "crc32", "crc32_batch", "crc32_combine",
-    "crc32_ragged_device", "crc32_shards_device", "crc32_uniform_device", "shard_bounds_native", "default_context", "insert_batch", "slot_adjust",
+    "crc32_ragged_device", "crc32_shards_device", "crc32_uniform_device", "shard_bounds_native", "default_context", "device_status", "insert_batch", "slot_adjust",
     "verify_batch", "RangeCoder", "compress_batch", "decompress_batch", "gather_slices",
 ]

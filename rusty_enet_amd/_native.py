@@ -24,6 +24,7 @@ ENET_CRC_E_INVALID = -1
 ENET_CRC_E_NO_DEVICE = -2
 ENET_CRC_E_HIP = -3
 ENET_CRC_E_NOMEM = -4
+ENET_CRC_E_DEVICE = -5  # a batch kernel gave up on the device: outputs invalid (ABI 6)
 
 
 class NativeLibraryMissing(RuntimeError):
@@ -61,6 +62,7 @@ _SIGNATURES = {
     "enet_crc_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "enet_crc_last_hip_error": (ctypes.c_int, []),
     "enet_crc_device_count": (ctypes.c_int, []),
+    "enet_crc_device_status": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "enet_crc_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "enet_crc_ctx_create_multi": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_uint32,
                                                  ctypes.POINTER(ctypes.c_void_p)]),
@@ -119,7 +121,7 @@ ENET_CRC_PERCALL_COPY = 0
 ENET_CRC_PERCALL_ZEROCOPY = 1
 ENET_CRC_PERCALL_PERSISTENT = 2
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 def lib() -> ctypes.CDLL:

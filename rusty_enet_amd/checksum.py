@@ -311,6 +311,20 @@ def _check_dev(dev, **tensors) -> None:
             raise ValueError(f"{name} must be contiguous")
 
 
+def device_status(device: int = 0, clear: bool = False) -> int:
+    """``enet_crc_device_status``: the device's failure bits (0 = none) since the last clear.
+
+    A batch kernel that gave up on an inter-wave wait sets them (include/enet_crc_amd.h);
+    after the asynchronous device entries (``crc32_batch``, ``verify_batch``, ...) a caller
+    that must not trust a failed batch synchronises and checks this.  The synchronous host
+    entries raise ``CrcError`` with ``ENET_CRC_E_DEVICE`` instead.
+    """
+    st = lib().enet_crc_device_status(int(device), 1 if clear else 0)
+    if st < 0:
+        check(st, "enet_crc_device_status")
+    return st
+
+
 def crc32_shards_device(shards: Sequence[dict]) -> None:
     """``enet_crc32_shards_device``: one batch per device, launched on every device at
     once.  Each shard is a dict with ``data`` (uint8 tensor) and either ``stride``/

@@ -66,6 +66,45 @@ hipError_t set_device_kick_word(uint32_t* d_word) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_kick_word), &d_word, sizeof(d_word));
 }
 
+// The device's failure word (device address of a mapped, coherent pinned host word): a
+// batch kernel that gives up on an inter-wave wait writes its kFault* bit here, so the
+// host sees it without a copy (enet_crc_device_status).  Set before the first launch of
+// the ragged jobs kernel on the device (device_fault_word below).
+__device__ uint32_t* g_fault_word = nullptr;
+
+namespace {
+constexpr int kMaxFaultDevices = 64;
+std::mutex g_fault_lock;
+uint32_t* g_fault_host[kMaxFaultDevices];  // host address of each device's word (never freed: 64 B)
+}  // namespace
+
+hipError_t device_fault_word(int dev, volatile uint32_t** host_word) {
+  if (dev < 0 || dev >= kMaxFaultDevices) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(g_fault_lock);
+  if (!g_fault_host[dev]) {
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return e;
+    if (cur != dev && (e = hipSetDevice(dev)) != hipSuccess) return e;
+    uint32_t* h = nullptr;
+    uint32_t* d = nullptr;
+    e = hipHostMalloc((void**)&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+      memset(h, 0, 64);
+      e = hipHostGetDevicePointer((void**)&d, h, 0);
+    }
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_fault_word), &d, sizeof(d));
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+      if (h) (void)hipHostFree(h);
+      return e;
+    }
+    g_fault_host[dev] = h;
+  }
+  *host_word = g_fault_host[dev];
+  return hipSuccess;
+}
+
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1066,8 +1105,10 @@ __global__ __launch_bounds__(kBlock) void crc32_wave_regs_kernel(UniformBatch u,
     return none0 || is_below(pb) ? c.dummy : pb + (uint64_t)rel0;
   };
   auto ld = [&](uint64_t a) -> u32x4 {
+    // kNT: every packet ends on a 128-B line, so each chunk is 16-B aligned; otherwise
+    // chunks are only 4-B aligned (a base at +4 or +12): the packed 4-B-aligned type.
     if constexpr (kNT) return __builtin_nontemporal_load(reinterpret_cast<GlobalU32x4W*>(a));
-    return *reinterpret_cast<GlobalU32x4W*>(a);
+    return load_chunk(a);
   };
   uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
   if (rnd0 >= total) return;
@@ -1588,6 +1629,10 @@ constexpr uint32_t kJobRecBytes = kJobRounds * kJobRoundBytes;   // 3 KiB, also 
 constexpr int kJobLidShift = 54;                                 // local id (0..255) in ax bits 54..61
 constexpr uint32_t kJobClassWords = 6;                           // 17 classes (16 = no packet), 3 x 10 bits
 constexpr uint32_t kJobSpinLimit = 1u << 22;                     // give up rather than hang (never hit)
+// Failure bits (g_fault_word, enet_crc_device_status): which wait gave up first in a wave.
+constexpr uint32_t kFaultReady = 1u;     // a job's records never became ready
+constexpr uint32_t kFaultConsumed = 2u;  // a job slot's previous job was never fully read
+constexpr uint32_t kFaultFreed = 4u;     // a result slot's previous job was never flushed
 static_assert(kJobPackets == 4 * 64, "4 packets per lane");
 static_assert(kJobRecBytes == kJobPackets * 12, "staging: u64 offsets + u32 lengths");
 
@@ -1604,6 +1649,7 @@ struct RaggedJobsLds {
   uint32_t done[kJobSlots];      // rounds of the job whose checksums are in res
   uint32_t freed[kJobSlots];     // k + 1 once the k-th job's checksums are in HBM
   uint32_t next_dispatch;
+  uint32_t failed;               // != 0 once a wave gave up a wait: later waits fail at once, nothing more is flushed
 };
 static_assert(sizeof(RaggedJobsLds) <= 160 * 1024, "LDS");
 
@@ -1614,6 +1660,9 @@ struct RaggedJobsBatch {
   uint64_t count;
   uint64_t njobs;
   uint32_t job_packets;  // packets per job (<= kJobPackets), chosen so every workgroup gets the same job count
+#ifdef ENET_CRC_TEST_HOOKS
+  uint32_t fault_k;  // test build: workgroup 0's (fault_k - 1)-th job reports its records never ready (0: none)
+#endif
 };
 
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t a) {
@@ -1654,13 +1703,29 @@ __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
 __device__ unsigned long long g_round_stamps[8];
 #endif
 
-// Spin (asleep) until the LDS word at `a` equals `want`; false after kJobSpinLimit polls.
-__device__ __forceinline__ bool lds_wait_eq(uint32_t a, uint32_t want) {
+// Spin (asleep) until the LDS word at `a` equals `want`.  kWaitOk, or kWaitGaveUp after
+// kJobSpinLimit polls, or kWaitFailFast as soon as the workgroup's failed word (at `fail`)
+// is set: one wave that gives up makes every later wait of its workgroup return at once,
+// so a broken pipeline drains in one pass instead of one time-out per round.
+enum : uint32_t { kWaitOk = 0, kWaitGaveUp = 1, kWaitFailFast = 2 };
+__device__ __forceinline__ uint32_t lds_wait_eq(uint32_t a, uint32_t want, uint32_t fail) {
   for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
-    if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) return true;
+    if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) return kWaitOk;
+    if (__builtin_amdgcn_readfirstlane(lds_ld32(fail)) != 0u) return kWaitFailFast;
     __builtin_amdgcn_s_sleep(2);
   }
-  return false;
+  return kWaitGaveUp;
+}
+
+// A wave gave up a wait: mark its workgroup failed (LDS) and write the failure bit into the
+// device's failure word in host memory (one vector store by lane 0, system scope, waited
+// for; a racing writer can only replace one non-zero bit by another).
+__device__ __forceinline__ void report_fault(uint32_t fail, uint32_t bit) {
+  if ((threadIdx.x & 63u) != 0u) return;
+  lds_st32(fail, bit);
+  uint32_t* const w = g_fault_word;
+  if (!w) return;
+  asm volatile("global_store_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : : "v"(w), "v"(bit) : "memory");
 }
 
 __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
@@ -1675,7 +1740,10 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     S.done[threadIdx.x] = 0;
     S.freed[threadIdx.x] = 0;
   }
-  if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * kLook;
+  if (threadIdx.x == 0) {
+    S.next_dispatch = kWavesPerBlock * kLook;
+    S.failed = 0;
+  }
   fill_lds(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
@@ -1801,6 +1869,12 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
 
   // Jobs this wave has seen ready / flushed (a job's flags are polled once per wave).
   uint32_t seen_ready = 0, seen_freed = 0;
+  const uint32_t fail_a = lds_addr(&S.failed);
+  // A wait's outcome: true if the flag came; a wave's own time-out is reported.
+  auto waited = [&](uint32_t w, uint32_t bit) -> bool {
+    if (w == kWaitGaveUp) report_fault(fail_a, bit);
+    return w == kWaitOk;
+  };
   auto make_round = [&](uint32_t d) -> RaggedRound {
     uint64_t ax = 0;
     uint32_t info = 0;
@@ -1810,9 +1884,12 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     const bool live = (d - k * RJ) * kPacketsPerWave < n;  // round_valid(d)
     bool rv = live;
     if (rv && k + 1u > seen_ready) {
-      rv = lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u);
+      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
       if (rv) seen_ready = k + 1u;
     }
+#ifdef ENET_CRC_TEST_HOOKS
+    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k) rv = waited(kWaitGaveUp, kFaultReady);
+#endif
     if (rv) {
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
       asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"  // one round trip
@@ -1856,7 +1933,8 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     bool build = false;
     const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
     if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
-      build = kb < (uint32_t)kJobSlots || lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ);
+      build = kb < (uint32_t)kJobSlots ||
+              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
       if (build) {
         if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
         job_dma(job_of(kb), bslot);
@@ -1889,7 +1967,7 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     // writes the job's checksums to HBM.
     const uint32_t k0 = cur.job_k, slot0 = k0 % kJobSlots;
     if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
-      if (lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u))
+      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
     }
     // The checksum store is not waited for on its own: the done counter's wait below covers
@@ -1898,7 +1976,9 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
     old = __builtin_amdgcn_readfirstlane(old);
-    if (old + 1u == cur.job_rounds) {
+    // After a failure in the workgroup nothing more is flushed: a job whose records or
+    // result slot were skipped would leave stale checksums in res[].
+    if (old + 1u == cur.job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
       const uint64_t J0 = job_of(k0);
       const uint32_t n0 = job_count(J0);
       const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
@@ -1910,6 +1990,8 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
         if (4u * lane + 1u < n0) dst[1] = v.y;
         if (4u * lane + 2u < n0) dst[2] = v.z;
       }
+    }
+    if (old + 1u == cur.job_rounds) {
       if (lane == 0) {
         lds_st32(lds_addr(&S.done[slot0]), 0u);
         lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
@@ -2149,7 +2231,25 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     }
   }
   const unsigned jblocks = (unsigned)(njobs < (uint64_t)cus ? njobs : (uint64_t)cus);
-  const RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
+  // The kernel divides a workgroup's round index by RJ with one s_mul_hi, exact below 2^27
+  // rounds (div_rj); a batch whose busiest workgroup would go past that (a device with few
+  // CUs and billions of packets) takes the streaming kernel instead.
+  const uint64_t wg_rounds = (njobs + jblocks - 1) / jblocks * (jp / kPacketsPerWave) + 2 * kWavesPerBlock;
+  if (wg_rounds >= (1ull << 27)) {
+    Launcher<true> L{b, out, stream, blocks};
+    return L.streaming();
+  }
+  // The kernel's failure channel must exist before its first launch on this device.
+  int dev = 0;
+  volatile uint32_t* fault = nullptr;
+  if ((err = hipGetDevice(&dev)) != hipSuccess || (err = device_fault_word(dev, &fault)) != hipSuccess) return err;
+  RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
+#ifdef ENET_CRC_TEST_HOOKS
+  // Test build only (tests/test_gpu_hooks.py): ENET_CRC_TEST_JOB_FAULT=k makes workgroup 0's
+  // (k-1)-th job report that its records never became ready.
+  const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
+  jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
+#endif
   hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
   return hipGetLastError();
 }

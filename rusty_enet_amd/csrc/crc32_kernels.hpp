@@ -38,4 +38,10 @@ int cu_count_for_current_device();
 // Registers the current device's kick word (enet_crc_abi.hip) with its batch kernels.
 hipError_t set_device_kick_word(uint32_t* d_word);
 
+// Host address of device `dev`'s failure word (mapped, coherent pinned memory; allocated
+// and registered with that device's kernels on first use).  Non-zero once a batch kernel
+// gave up on an inter-wave wait (crc32_ragged_jobs_kernel: kFault* bits); sticky until
+// the host writes 0.  launch_ragged calls it before every launch.
+hipError_t device_fault_word(int dev, volatile uint32_t** host_word);
+
 }  // namespace enet_crc

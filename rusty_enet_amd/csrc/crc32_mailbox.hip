@@ -113,16 +113,20 @@ __global__ __launch_bounds__(64) void crc32_mailbox_kernel(const Mailbox* req, M
     seq = __builtin_amdgcn_readfirstlane(seq);
     len = __builtin_amdgcn_readfirstlane(len);
     k = __builtin_amdgcn_readfirstlane(k);
-    if (seq == kMailboxStop || k != kick0) break;  // stop request, or a batch launch wants the CU
-    const uint64_t now = wall_clock64();
 #ifdef ENET_CRC_TEST_HOOKS
-    // Test build only: a 4095-byte request is never answered (the host's timeout path).
-    const bool ignore = len == 4095u;
+    // Test build only: a 4095-byte request is never answered (the host's timeout path); after
+    // a 4094-byte request the wave is deaf to stop requests, kicks and its idle limit too and
+    // runs until its 2-s lifetime ends (the host's bounded stop and leak path).
+    const bool deaf = len == 4094u;
+    const bool ignore = len == 4095u || deaf;
 #else
+    constexpr bool deaf = false;
     constexpr bool ignore = false;
 #endif
+    if ((seq == kMailboxStop || k != kick0) && !deaf) break;  // stop request, or a batch launch wants the CU
+    const uint64_t now = wall_clock64();
     if (seq == last || ignore) {
-      if (now - t_last > kMailboxIdleTicks || now - t0 > kMailboxMaxTicks) break;
+      if ((now - t_last > kMailboxIdleTicks && !deaf) || now - t0 > kMailboxMaxTicks) break;
       __builtin_amdgcn_s_sleep(2);
       continue;
     }

@@ -83,6 +83,18 @@ int stream_device(hipStream_t s) {
   return hipStreamGetDevice(s, &d) == hipSuccess ? d : -1;
 }
 
+// The device-side failure channel (crc32_kernels.hpp: device_fault_word): ENET_CRC_E_DEVICE
+// if a batch kernel on `dev` gave up since the word was last cleared (the word is cleared).
+// The synchronous entries call it after their last wait.
+int take_device_fault(int dev) {
+  volatile uint32_t* w = nullptr;
+  const hipError_t e = device_fault_word(dev, &w);
+  if (e != hipSuccess) return fail_hip(e);
+  if (*w == 0u) return ENET_CRC_OK;
+  (void)__atomic_exchange_n(const_cast<uint32_t*>(w), 0u, __ATOMIC_ACQ_REL);
+  return ENET_CRC_E_DEVICE;
+}
+
 }  // namespace
 
 // Operator ladder of the slot correction and the flat ragged kernel's finish pass
@@ -263,6 +275,7 @@ struct PerCall {
   hipStream_t mb_stream = nullptr;
   int mb_device = 0;          // device of mb_stream (lane 0's)
   bool mb_launched = false;   // a server was launched and may still run
+  bool mb_wedged = false;     // a stop request was not honoured within kServerStopLimit
   uint32_t mb_seq = 0;        // last request number posted
 };
 
@@ -361,11 +374,15 @@ struct enet_crc_ring {
 
 namespace {
 
-// A persistent-mode call gives up on the server after this long (test build: 200 ms).
+// A persistent-mode call gives up on the server after this long (test build: 200 ms), and
+// a stop request waits at most kServerStopLimit for the server's stream to drain (longer
+// than the server's 2-s lifetime, so only a wedged wave misses it; test build: 100 ms).
 #ifdef ENET_CRC_TEST_HOOKS
 constexpr std::chrono::milliseconds kMailboxCallTimeout(200);
+constexpr std::chrono::milliseconds kServerStopLimit(100);
 #else
 constexpr std::chrono::milliseconds kMailboxCallTimeout(5000);
+constexpr std::chrono::milliseconds kServerStopLimit(3000);
 #endif
 
 // Host path chunking: at most this many staged bytes / packets per slot.
@@ -452,7 +469,7 @@ int ragged_host_shard(Lane& L, const uint8_t* base, const uint64_t* h_offsets, c
   }
   for (auto& s : L.slot) ENET_TRY(drain(s));
   guard.armed = false;
-  return ENET_CRC_OK;
+  return take_device_fault(L.device);
 }
 
 void destroy_lane(Lane& L) {
@@ -494,11 +511,25 @@ const char* enet_crc_strerror(int status) {
     case ENET_CRC_E_NO_DEVICE: return "no usable HIP device";
     case ENET_CRC_E_HIP: return "HIP runtime error";
     case ENET_CRC_E_NOMEM: return "out of memory";
+    case ENET_CRC_E_DEVICE: return "a batch kernel gave up on the device (outputs invalid)";
     default: return "unknown status";
   }
 }
 
 int enet_crc_last_hip_error(void) { return t_last_hip_error; }
+
+int enet_crc_device_status(int device, int clear) {
+  int n = 0;
+  const hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return e == hipSuccess || e == hipErrorNoDevice ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
+  if (device < 0 || device >= n) return ENET_CRC_E_NO_DEVICE;
+  volatile uint32_t* w = nullptr;
+  const hipError_t fe = device_fault_word(device, &w);
+  if (fe != hipSuccess) return fail_hip(fe);
+  const uint32_t v = clear ? __atomic_exchange_n(const_cast<uint32_t*>(w), 0u, __ATOMIC_ACQ_REL)
+                           : __atomic_load_n(const_cast<uint32_t*>(w), __ATOMIC_ACQUIRE);
+  return (int)(v & 0x7FFFFFFFu);
+}
 
 int enet_crc_device_count(void) {
   int n = 0;
@@ -554,29 +585,30 @@ int enet_crc_ctx_lanes(const enet_crc_ctx* ctx) { return ctx ? (int)ctx->lanes.s
 
 namespace {
 
-// Ask a running server to exit and wait until it has (its stream drains).
-void stop_mailbox(PerCall& c) {
-  if (!c.mb_launched) return;
-  __atomic_store_n(&c.req->seq, kMailboxStop, __ATOMIC_RELEASE);
-  __builtin_ia32_sfence();
-  (void)hipStreamSynchronize(c.mb_stream);
-  set_server_live(c, false);
-}
-
-// After a request timed out: ask the server to exit and wait for its stream at most
-// `limit`.  Returns whether it drained (if not, the wave stays counted as resident).
+// Ask a running server to exit and wait for its stream at most `limit`.  Returns whether
+// it drained; if not, the wave stays counted as resident and is marked wedged: later stops
+// only re-check it (no second wait), persistent calls fail at once, and destroy leaks the
+// stream and mailbox memory the wave may still touch instead of hanging on it.
 bool stop_mailbox_bounded(PerCall& c, std::chrono::milliseconds limit) {
   if (!c.mb_launched) return true;
+  if (c.mb_wedged) limit = std::chrono::milliseconds(0);
   __atomic_store_n(&c.req->seq, kMailboxStop, __ATOMIC_RELEASE);
   __builtin_ia32_sfence();
   const auto t0 = std::chrono::steady_clock::now();
   while (hipStreamQuery(c.mb_stream) == hipErrorNotReady) {
-    if (std::chrono::steady_clock::now() - t0 > limit) return false;
+    if (std::chrono::steady_clock::now() - t0 >= limit) {
+      c.mb_wedged = true;
+      return false;
+    }
     std::this_thread::sleep_for(std::chrono::microseconds(100));
   }
   set_server_live(c, false);
+  c.mb_wedged = false;
   return true;
 }
+
+// Ask a running server to exit and wait until it has (bounded by kServerStopLimit).
+void stop_mailbox(PerCall& c) { (void)stop_mailbox_bounded(c, kServerStopLimit); }
 
 }  // namespace
 
@@ -620,6 +652,14 @@ void enet_crc_ctx_destroy(enet_crc_ctx* ctx) {
     DeviceGuard g(ctx->lanes[0].device);
     stop_mailbox(ctx->call);
   }
+  if (ctx->call.mb_launched) {
+    // The server wave ignored the stop request (mb_wedged).  Every free below would wait
+    // for the device, i.e. for that wave: leak the context's device and pinned memory and
+    // its streams instead of hanging (the worker threads are still joined).
+    for (auto& L : ctx->lanes) L.worker.reset();
+    delete ctx;
+    return;
+  }
   for (auto& L : ctx->lanes) destroy_lane(L);
   if (!ctx->lanes.empty()) {
     DeviceGuard g(ctx->lanes[0].device);
@@ -652,12 +692,39 @@ int enet_crc32_ragged_device(const void* d_base, const uint64_t* d_offsets, cons
   return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
 }
 
+namespace {
+
+// Whether `p` is device memory of device `dev` (any address inside a hipMalloc'd block).
+bool on_device(const void* p, int dev) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // an unregistered host pointer: not device memory
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice && a.device == dev;
+}
+
+}  // namespace
+
 int enet_crc32_shards_device(const enet_crc_shard* shards, size_t nshards) {
   if (nshards > 0 && !shards) return ENET_CRC_E_INVALID;
+  int ndev = 0;
+  if (nshards > 0) {
+    const hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) return e == hipSuccess || e == hipErrorNoDevice ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
+  }
+  // Placement is checked for every shard before anything launches: each shard's buffers
+  // and stream must belong to its own device (a misplaced shard would otherwise run as
+  // peer reads across the fabric, or fault).
   for (size_t i = 0; i < nshards; ++i) {
     const enet_crc_shard& s = shards[i];
     if (s.count == 0) continue;
     if (!s.d_out || !s.d_base || (s.d_offsets != nullptr) != (s.d_lengths != nullptr)) return ENET_CRC_E_INVALID;
+    if (s.device < 0 || s.device >= ndev) return ENET_CRC_E_NO_DEVICE;
+    if (!on_device(s.d_base, s.device) || !on_device(s.d_out, s.device) ||
+        (s.d_offsets && (!on_device(s.d_offsets, s.device) || !on_device(s.d_lengths, s.device))))
+      return ENET_CRC_E_INVALID;
+    if (s.hip_stream && stream_device(static_cast<hipStream_t>(s.hip_stream)) != s.device) return ENET_CRC_E_INVALID;
   }
   for (size_t i = 0; i < nshards; ++i) {
     const enet_crc_shard& s = shards[i];
@@ -753,6 +820,9 @@ int enet_crc32_iov(enet_crc_ctx* ctx, const enet_crc_iov* bufs, size_t nbufs, ui
         c.d_req = c.d_mb;
       }
     }
+    // A server that ignored a stop request still owns the mailbox: fail at once (until
+    // its stream drains) rather than post into it and wait for the call time-out.
+    if (c.mb_wedged && !stop_mailbox_bounded(c, std::chrono::milliseconds(0))) return fail_hip(hipErrorLaunchTimeOut);
     const uint32_t* ladder = nullptr;
     ENET_HIP_TRY(device_slot_ladder(&ladder));
     uint8_t* dst = c.req->data + (kMailboxBytes - total);  // right-aligned; zero below it in its chunk
@@ -983,9 +1053,11 @@ int enet_crc_ring_wait(enet_crc_ring* r, uint32_t slot) {
   }
   DeviceGuard g(r->device);
   const hipError_t e = hipEventSynchronize(s.done);
-  std::lock_guard<std::mutex> lk(r->lock);
-  s.busy = false;
-  return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+  {
+    std::lock_guard<std::mutex> lk(r->lock);
+    s.busy = false;
+  }
+  return e == hipSuccess ? take_device_fault(r->device) : fail_hip(e);
 }
 
 }  // extern "C"

@@ -1,0 +1,16 @@
+#!/usr/bin/env python3
+"""Print the key numbers of bench.py JSON lines (tooling)."""
+import json
+import sys
+
+for path in sys.argv[1:]:
+    with open(path) as f:
+        line = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
+    r = line["roofline"]
+    print(f"{path}: value {line['value']} GiB/s, kernel {r['kernel_ms'] * 1000:.1f} us, frac {r['frac']}, "
+          f"ceiling {r.get('read_ceiling_gbs')} GB/s, frac_of_ceiling {r.get('frac_of_ceiling')}")
+    for k in ("shard_2m", "mtu_1392", "ragged_g2", "large_64k", "frag_64k"):
+        if k in line:
+            p = line[k]
+            print(f"  {k:10s} kernel {p['kernel_ms'] * 1000:7.1f} us  frac {p['frac']:.4f}  "
+                  f"ceiling {p.get('read_ceiling_gbs')}  frac_of_ceiling {p.get('frac_of_ceiling')}")

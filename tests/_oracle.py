@@ -47,6 +47,9 @@ def lib() -> ctypes.CDLL:
             h.oracle_crc32_uniform.restype = None
             h.oracle_crc32_uniform.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                ctypes.c_uint64, ctypes.c_void_p]
+            h.oracle_crc32_ragged_mt.restype = ctypes.c_int
+            h.oracle_crc32_ragged_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
             h.oracle_crc32_uniform_mt.restype = ctypes.c_int
             h.oracle_crc32_uniform_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
@@ -72,12 +75,17 @@ def crc32(slices) -> int:
     return lib().oracle_crc32_iov(iov, len(arrs))
 
 
-def crc32_ragged(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
+def crc32_ragged(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, threads: int = 1) -> np.ndarray:
     data = np.ascontiguousarray(data, dtype=np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    assert off.size == 0 or int((off + ln).max()) <= data.size
     out = np.empty(off.size, dtype=np.uint32)
-    lib().oracle_crc32_ragged(data.ctypes.data, off.ctypes.data, ln.ctypes.data, off.size, out.ctypes.data)
+    if threads > 1:
+        assert lib().oracle_crc32_ragged_mt(data.ctypes.data, off.ctypes.data, ln.ctypes.data, off.size,
+                                            out.ctypes.data, threads) == 0
+    else:
+        lib().oracle_crc32_ragged(data.ctypes.data, off.ctypes.data, ln.ctypes.data, off.size, out.ctypes.data)
     return out
 
 

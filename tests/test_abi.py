@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
     lib = _native.lib()
     for name in _declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.enet_crc_abi_version() == _native.ABI_VERSION == 5
+    assert lib.enet_crc_abi_version() == _native.ABI_VERSION == 6
     assert lib.enet_crc_strerror(0) == b"ok"
     assert lib.enet_crc_strerror(_native.ENET_CRC_E_NO_DEVICE) == b"no usable HIP device"
 

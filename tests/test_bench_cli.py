@@ -58,3 +58,27 @@ def test_traffic_is_dropped_when_kernel_sources_change(tmp_path, monkeypatch):
 def test_host_cpus_reports_model_and_threads():
     c = bench.host_cpus()
     assert c["threads"] >= 1 and c["nproc"] >= 1 and isinstance(c["model"], str)
+
+
+def test_ceiling_fields_frac_of_ceiling():
+    """roofline.frac_of_ceiling = the kernel's algorithmic GB/s / the read ceiling measured
+    right after the timed steps with the variant that was best before them."""
+    import bench
+
+    class FakeCeil:
+        def __init__(self):
+            self.calls = []
+
+        def measure(self, data, nbytes, launches=10, variants=None):
+            self.calls.append((launches, variants))
+            return {"gbs": 6400.0, "variant": "nt", "variant_index": 2, "bytes": nbytes, "launches": launches,
+                    "variants": {"nt": {"us": 1.0, "gbs": 6400.0}}}
+
+    c = FakeCeil()
+    pre = {"gbs": 6500.0, "variant": "nt", "variant_index": 2, "variants": {"nt": {"us": 1.0, "gbs": 6500.0}}}
+    f = bench.ceiling_fields(c, pre, None, 1 << 20, 6000.0)
+    assert c.calls == [(20, [2])]
+    assert f["read_ceiling_gbs"] == 6400.0 and f["frac_of_ceiling"] == round(6000.0 / 6400.0, 4)
+    assert f["read_ceiling"]["before_gbs"] == 6500.0 and f["read_ceiling"]["variant"] == "nt"
+    none = bench.ceiling_fields(None, None, None, 1, 1.0)
+    assert none["read_ceiling_gbs"] is None and none["frac_of_ceiling"] is None

@@ -44,6 +44,7 @@ def _rank(rank: int, world: int, port: int, outdir: str) -> None:
 
     bench.make_workload = make_workload
     bench.verify_sample = lambda out, spec, limit=20000: None
+    bench.open_ceiling = lambda dev: None  # the read-ceiling probe needs a GPU
     bench.time_steps = time_steps
     bench.device_record = lambda dev, r: {"rank": r, "device": dev.index, "pci": f"0000:{0x10 * (r + 1):02x}:00"}
     buf = io.StringIO()
@@ -75,6 +76,7 @@ def test_multi_gpu_line_shape(tmp_path):
     assert big["ms_per_step"] == pytest.approx(2.0) and big["kernel_ms"] == pytest.approx(1.8)
     assert big["value"] == pytest.approx(2 * 32768 * 65536 / 2e-3 / 2**30, rel=1e-3)
     assert big["frac"] == pytest.approx(32768 * 65536 / 1.8e-3 / 1e9 / 8000.0, rel=1e-3)
+    assert line["roofline"]["read_ceiling_gbs"] is None and "not built" in line["roofline"]["read_ceiling"]["note"]
     devs = line["devices"]
     assert [d["rank"] for d in devs] == [0, 1] and [d["device"] for d in devs] == [0, 1]
     assert len({d["pci"] for d in devs}) == 2

@@ -92,6 +92,48 @@ def test_shards_device_two_shards(dev):
     assert digest == _oracle.crc32([a])
 
 
+def test_shards_device_rejects_misplaced_shards(dev):
+    """enet_crc32_shards_device checks every shard's placement before
+    anything launches.  A shard naming another device than the one its buffers live on
+    (E_INVALID; on a 1-GPU box the index itself is bad: E_NO_DEVICE), a shard whose input
+    or output is host memory, or whose stream belongs to another device, fails the whole
+    call, and the valid shard in front of it does not run."""
+    n, L = 4096, 1200
+    a = torch.from_numpy(splitmix64_bytes(51, n * L)).to(dev)
+    oa = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    ob = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    host_out = torch.zeros(n, dtype=torch.int32).pin_memory()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def shard(device, base, out, s=stream):
+        sh = _native.Shard()
+        sh.device, sh.d_base, sh.d_offsets, sh.d_lengths = device, base, None, None
+        sh.stride, sh.length, sh.count, sh.d_out, sh.hip_stream = L, L, n, out, s
+        return sh
+
+    lib = _native.lib()
+    ndev = torch.cuda.device_count()
+    bad_dev_status = _native.ENET_CRC_E_INVALID if ndev > 1 else _native.ENET_CRC_E_NO_DEVICE
+    cases = [
+        (shard(1, a.data_ptr(), ob.data_ptr()), bad_dev_status),           # pointers on device 0
+        (shard(0, a.data_ptr(), host_out.data_ptr()), _native.ENET_CRC_E_INVALID),  # output in host memory
+        (shard(0, host_out.data_ptr(), ob.data_ptr()), _native.ENET_CRC_E_INVALID),  # input in host memory
+        (shard(-1, a.data_ptr(), ob.data_ptr()), _native.ENET_CRC_E_NO_DEVICE),
+    ]
+    if ndev > 1:
+        s1 = torch.cuda.Stream(device=torch.device("cuda", 1))
+        cases.append((shard(0, a.data_ptr(), ob.data_ptr(), s1.cuda_stream), _native.ENET_CRC_E_INVALID))
+    for bad, status in cases:
+        arr = (_native.Shard * 2)(shard(0, a.data_ptr(), oa.data_ptr()), bad)
+        assert lib.enet_crc32_shards_device(arr, 2) == status
+        torch.cuda.synchronize()
+        assert bool((oa == 7).all()) and bool((ob == 7).all())  # nothing launched
+    arr = (_native.Shard * 1)(shard(0, a.data_ptr(), oa.data_ptr()))
+    assert lib.enet_crc32_shards_device(arr, 1) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(oa.cpu().numpy().view(np.uint32), _oracle.crc32_uniform(a.cpu().numpy(), L, L, n))
+
+
 @pytest.mark.parametrize("mode", [_native.ENET_CRC_PERCALL_COPY, _native.ENET_CRC_PERCALL_ZEROCOPY,
                                   _native.ENET_CRC_PERCALL_PERSISTENT])
 def test_per_call_modes(dev, mode):

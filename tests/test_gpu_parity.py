@@ -196,6 +196,27 @@ def test_full_shard_large_32768_x_64k(dev):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("base", [0, 1])
+def test_full_size_frag_64k_datagrams(dev, base):
+    """the configs[4] bytes as the reference checksums them (bench.py's
+    `frag_64k`): 32,768 payloads of 64 KiB, each fragmented at the default MTU into 48
+    datagrams of 1392 B and one of 288 B (src/c/peer.rs:181-192), packed back to back from
+    `base`: all 1,605,632 datagrams against the oracle (16 threads)."""
+    n = 32768
+    lengths = np.tile(np.array([1392] * 48 + [288], dtype=np.uint32), n)
+    offsets = packed_offsets(lengths) + np.uint64(base)
+    total = int(lengths.sum()) + base
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED + 5 + base)
+    d = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    got = as_u32(rea.crc32_batch(d, offsets=to_dev(offsets.astype(np.int64), dev),
+                                 lengths=to_dev(lengths.astype(np.int32), dev)))
+    want = _oracle.crc32_ragged(d.cpu().numpy(), offsets, lengths, threads=16)
+    del d
+    assert got.size == lengths.size == 1_605_632
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+
+
 # --- properties --------------------------------------------------------------------
 
 def test_single_bit_flips_are_detected(dev):
