@@ -253,6 +253,7 @@ constexpr uint32_t kMetaNTailShift = 6;       // 2 bits: trailing bytes (0..3)
 constexpr uint32_t kMetaTShiftShift = 8;      // 2 bits: first trailing byte's position in its word
 constexpr uint32_t kMetaStore = 1u << 10;     // packet index < count
 constexpr uint32_t kMetaFallback = 1u << 11;  // top chunk begins before the caller's buffer
+constexpr uint32_t kMetaDirect = 1u << 12;    // ragged rounds: the top chunk is read directly (inside, no fallback)
 
 __device__ __forceinline__ uint32_t round_meta(const PacketGeo& g, uint32_t k, uint64_t base4, bool store,
                                                uint64_t& tail_addr, uint64_t dummy) {
@@ -1442,12 +1443,12 @@ struct RaggedRound {
   uint32_t meta;        // round_meta(); the trailing-byte field holds z (bytes run past the end)
   uint32_t id;          // packet id (output index)
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
-  bool direct;          // top chunk read directly (not fallback / not before the packet)
   bool fast;            // wave-uniform: every lane's top is the same slot, no fallback, ns <= kRaggedFastMax
   bool live;            // jobs kernel: the round is inside the batch (wave-uniform)
   uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
   uint32_t job_rounds;  // jobs kernel: rounds of that job
   int32_t top_uniform;  // that slot (0 unless ns == kRaggedRing and the packets are shorter)
+  int32_t spread;       // 16-packet rounds: max - min step count of the round's packets (wave-uniform)
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
@@ -1476,10 +1477,9 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
     const uint64_t top = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
     fb = top - c.base4 < (uint64_t)(-rel);
   }
-  rr.direct = inside && !fb;
   const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
   rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
-            (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u);
+            (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
   rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
   rr.id = id;
   // Fast: every packet starts at the same slot (same step count), no fallback chunk,
@@ -1491,10 +1491,12 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   return rr;
 }
 
-// Source of this lane's slot-s DMA in round rr (the zero chunk before its top).
+// Source of this lane's slot-s DMA in round rr (the zero chunk before its top); kStep bytes
+// per packet per slot (128: 8 lanes per packet, 64: 4 lanes).
+template <uint32_t kStep = kBytesPerStep>
 __device__ __forceinline__ uint64_t ragged_src(const RaggedRound& rr, int32_t s, uint64_t dummy) {
-  const bool real = s > rr.top_slot || (s == rr.top_slot && rr.direct);
-  return real ? rr.cb + (uint64_t)kBytesPerStep * (uint64_t)s : dummy;
+  const bool real = s > rr.top_slot || (s == rr.top_slot && (rr.meta & kMetaDirect));
+  return real ? rr.cb + (uint64_t)kStep * (uint64_t)s : dummy;
 }
 
 // Shared state of one wave's LDS-DMA ring (crc32_ragged_jobs_kernel).
@@ -1569,18 +1571,19 @@ __device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRo
 }
 
 // Any round (mixed step counts, fallback chunks, long packets): per-lane top slot.
+template <uint32_t kStep = kBytesPerStep>
 __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
                                                      const LaneConsts& c, const uint32_t* lds, uint32_t& h0,
                                                      uint32_t& h1, uint32_t& h2, uint32_t& h3) {
   for (int32_t s = 0; s < cur.ns; ++s) {
     const u32x4 v = R.nextv;
     const int32_t f = s + kRaggedRing;
-    R.dma(f < cur.ns ? ragged_src(cur, f, c.dummy) : ragged_src(nxt, f - cur.ns, c.dummy));
+    R.dma(f < cur.ns ? ragged_src<kStep>(cur, f, c.dummy) : ragged_src<kStep>(nxt, f - cur.ns, c.dummy));
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     const bool top = s == cur.top_slot;
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
       if (top && (cur.meta & kMetaFallback))
-        load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
+        load_top_words(cur.cb + (uint64_t)kStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
     }
     if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
@@ -1728,7 +1731,7 @@ __device__ __forceinline__ void report_fault(uint32_t fail, uint32_t bit) {
   asm volatile("global_store_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : : "v"(w), "v"(bit) : "memory");
 }
 
-__global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_jobs_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
   send_servers_home();
   constexpr int kDmaRing = kRaggedRing;
   __shared__ __attribute__((aligned(16))) RaggedJobsLds S;
@@ -2029,6 +2032,594 @@ __global__ __launch_bounds__(kBlock) void crc32_ragged_jobs_kernel(RaggedJobsBat
   __builtin_amdgcn_s_waitcnt(0);
 }
 
+
+// ---------------------------------------------------------------------------------
+// Ragged kernel with rounds of 16 packets, 4 lanes per packet (the default ragged path
+// since round 4).  Same pipeline as crc32_ragged_jobs_kernel above (jobs sorted by step
+// class in LDS, the LDS-DMA ring, dynamic round dispatch inside the workgroup, results
+// flushed per job, the failure channel), but a group of FOUR lanes owns a packet and a
+// slot covers 64 B of it: a round carries twice the bytes for the same per-round work
+// (record decode, combine, result, flags, dispatch), which is what bound the 8-lane
+// kernel (DESIGN.md §4 "Ragged jobs kernel": instruction issue, ~250 VALU + ~300 SALU
+// of fixed work per round).
+//   * Arithmetic: chunk c (16 B, from the packet end) belongs to lane k = c % 4 at step
+//     i = c / 4; Horner operator M32^16 (the replicated block's main set); in-lane
+//     combine as before; a 2-level tree M32^4, M32^8 across the 4 lanes.
+//   * Jobs of up to 512 packets (8 per lane of the building wave) sorted by 64-B step
+//     count (classes 0..23; 24 = longer, or a chunk that may reach below the caller's
+//     buffer).  The build writes a header per round: the smallest and largest step count
+//     of its 16 packets, and whether it needs the generic body.  A round's slot count
+//     then needs no cross-lane reduction.
+//   * Round bodies: unrolled for rounds of <= 23 slots whose packets differ by <= 2 steps
+//     (after the sort, nearly all).  Every lane's top slot lies in the first three
+//     slots; there each lane masks its own top chunk (exec-masked).  Other rounds take
+//     the generic loop.
+// ---------------------------------------------------------------------------------
+constexpr int kG4 = 4;                                   // lanes per packet
+constexpr int kPW4 = 64 / kG4;                           // packets per round
+constexpr uint32_t kStep4 = 16u * kG4;                   // bytes per packet per slot
+constexpr int kLevel4 = ilog2(4 * kG4);                  // Horner operator M32^16
+constexpr int kJobPackets4 = 512;                        // 8 per lane of the building wave
+constexpr int kJobRounds4 = kJobPackets4 / kPW4;         // 32
+constexpr int kJobSlots4 = 4;                            // job slots in LDS
+constexpr int kJobAhead4 = 2;                            // jobs built ahead of the one claimed
+constexpr uint32_t kRound4Bytes = 192;                   // per round: u64 ax[16], u32 info[16]
+constexpr uint32_t kRec4Bytes = kJobRounds4 * kRound4Bytes;  // 6 KiB, also the descriptor staging
+constexpr uint32_t kClassLong4 = 24;                     // class = step count below 24; 24: the rest
+constexpr uint32_t kClassNone4 = 25;                     // no packet
+constexpr int kFast4Max = (int)kClassLong4 - 1;          // unrolled bodies up to 23 slots (1472 B)
+constexpr uint32_t kHeadGeneric = 1u << 16;              // round header bit: generic body
+constexpr int kJobLidShift4 = 54;                        // local id (0..511) in ax bits 54..62
+static_assert(kRec4Bytes == kJobPackets4 * 12, "staging: u64 offsets + u32 lengths");
+static_assert((kJobSlots4 & (kJobSlots4 - 1)) == 0, "slot = job & (slots - 1)");
+static_assert(kRaggedRing == 3, "top slots 0..2 are issued by the previous round");
+
+struct JobSlot4 {
+  u32x4 rec[kRec4Bytes / 16];
+  uint32_t head[kJobRounds4];  // per round: min steps | max steps << 8 | kHeadGeneric
+  uint32_t hist[32];           // job build: packets per class, then each class's first position
+  uint32_t res[kJobPackets4];
+};
+struct Ragged16Lds {
+  uint32_t tables[kRepDwords + 2 * 1024];  // replicated M32^16 | M32^1 block, then M32^4 and M32^8
+  u32x4 ring[kRaggedRing][kWavesPerBlock][64];
+  JobSlot4 job[kJobSlots4];
+  uint32_t ready[kJobSlots4];     // k + 1 once the workgroup's k-th job has its records here
+  uint32_t consumed[kJobSlots4];  // rounds of the slot's job whose records have been read
+  uint32_t done[kJobSlots4];      // rounds of the job whose checksums are in res
+  uint32_t freed[kJobSlots4];     // k + 1 once the k-th job's checksums are in HBM
+  uint32_t next_dispatch;
+  uint32_t failed;                // != 0 once a wave gave up a wait (report_fault)
+};
+static_assert(sizeof(Ragged16Lds) <= 160 * 1024, "LDS");
+
+__device__ __forceinline__ void fill_lds4(uint32_t* lds) {
+  fill_replicated(lds, kLevel4);
+  for (int x = threadIdx.x; x < 2 * 1024; x += kBlock) {
+    const int set = x >> 10, rem = x & 1023;  // set l: M32^(4 * 2^l)
+    lds[kRepDwords + x] = g_op_tables.op[set + 2][rem >> 8][rem & 255];
+  }
+}
+
+// ragged_record for 64-B steps: nsteps = ceil(nwords / 16), pad = 64 nsteps - 4 nwords
+// (0..60); same ax / info fields.
+__device__ __forceinline__ RaggedRecord ragged_record4(uint64_t sa, uint32_t len, uint64_t base4) {
+  const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
+  const uint64_t a1 = sa + len + z, top = sa & ~(uint64_t)3;
+  const uint32_t nwords = (uint32_t)((a1 - top) >> 2);
+  const uint32_t nsteps = (nwords + 15u) >> 4;
+  const uint32_t pad = kStep4 * nsteps - 4u * nwords;
+  const uint64_t near = top - base4 < 16 ? 1ull : 0ull;
+  RaggedRecord r;
+  r.ax = a1 | ((sa & 3u) << kRecVShift) | ((uint64_t)z << kRecZShift) | (near << kRecNearBit) | (1ull << kRecValidBit);
+  r.info = nsteps | ((pad >> 2) << kRecPadShift);
+  r.nsteps = nsteps;
+  return r;
+}
+
+// Per-lane round state from the group's record and the round header (hdr, wave-uniform).
+__device__ __forceinline__ RaggedRound round16_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t hdr,
+                                                           const LaneConsts& c) {
+  const uint32_t k = threadIdx.x & (kG4 - 1);
+  const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
+  const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
+  const uint32_t pad = (info >> kRecPadShift) << 2;
+  const uint32_t v = valid ? (uint32_t)(ax >> kRecVShift) & 3u : 0u;
+  const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
+  const int32_t nsmin = (int32_t)(hdr & 255u), nsmax = (int32_t)((hdr >> 8) & 255u);
+  const bool generic = (hdr & kHeadGeneric) != 0u || nsmax == 0;
+  int32_t mx = nsmax;
+  if (generic) {  // rare: the header does not bound the round
+    mx = __builtin_amdgcn_readlane(nsteps, 0);
+#pragma unroll
+    for (int g = 1; g < kPW4; ++g) mx = max(mx, __builtin_amdgcn_readlane(nsteps, g * kG4));
+  }
+  RaggedRound rr;
+  rr.ns = max(kRaggedRing, mx);
+  rr.cb = a1 - 16u * (uint64_t)(k + 1u) - (uint64_t)kStep4 * (uint64_t)(rr.ns - 1);
+  rr.top_slot = rr.ns - nsteps;
+  // This lane's chunk at the top step, relative to top: 4 nwords - 16 (k + 4 (nsteps - 1) + 1)
+  // = 48 - 16 k - pad.
+  const int32_t rel = 48 - 16 * (int32_t)k - (int32_t)pad;
+  const bool inside = nsteps > 0 && rel > -16;
+  bool fb = false;
+  if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
+    const uint64_t top = a1 - ((uint64_t)kStep4 * (uint64_t)nsteps - pad);
+    fb = top - c.base4 < (uint64_t)(-rel);
+  }
+  const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
+  rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
+            (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
+  rr.last_mask = k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+  rr.id = (uint32_t)(ax >> kJobLidShift4) & (uint32_t)(kJobPackets4 - 1);
+  rr.top_uniform = rr.ns - nsmax;  // B: the first top slot of a fast round
+  rr.spread = nsmax - nsmin;
+  rr.fast = !generic && rr.ns <= kFast4Max && (rr.ns == kRaggedRing || rr.spread <= 2);
+  return rr;
+}
+
+// The LDS-DMA ring of crc32_ragged16_kernel (3 KiB per wave, 1 KiB per position), with its
+// positions in consumption order: slot s of the current round lands in position a[s % 3].
+// Unrolled bodies index it with their compile-time slot number, so a slot costs no ring
+// arithmetic (one M0 write); at a round's end the order rotates by the round's slot count.
+struct Ring3 {
+  uint32_t a0, a1, a2;  // wave-uniform LDS byte addresses
+  uint32_t lane16;      // lane * 16
+  u32x4 nextv;          // landed data of the slot about to be consumed
+  template <int S>
+  __device__ __forceinline__ uint32_t at() const {
+    return S % 3 == 0 ? a0 : (S % 3 == 1 ? a1 : a2);
+  }
+  __device__ __forceinline__ uint32_t at_rt(uint32_t m) const { return m == 0 ? a0 : (m == 1 ? a1 : a2); }
+  __device__ __forceinline__ void rotate(uint32_t r) {  // r = slots consumed, mod 3
+    const uint32_t b0 = a0, b1 = a1, b2 = a2;
+    a0 = r == 0 ? b0 : (r == 1 ? b1 : b2);
+    a1 = r == 0 ? b1 : (r == 1 ? b2 : b0);
+    a2 = r == 0 ? b2 : (r == 1 ? b0 : b1);
+  }
+};
+
+// One 16-B LDS-DMA per lane into the ring position at LDS byte address `lds`; kOff is the
+// instruction's immediate offset (no address arithmetic per slot).
+template <uint32_t kOff = 0>
+__device__ __forceinline__ void dma16(uint64_t src, uint32_t lds) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)(uintptr_t)lds, 16, kOff, 0);
+}
+
+// Source of slot f of round rr (64-B steps) as base + kOff: the zero chunk before the lane's
+// top (base = dummy - kOff), its chunk from there on.
+template <uint32_t kOff>
+__device__ __forceinline__ uint64_t ragged16_base(const RaggedRound& rr, int32_t f, uint64_t dummy) {
+  const bool real = f > rr.top_slot || (f == rr.top_slot && (rr.meta & kMetaDirect));
+  return real ? rr.cb : dummy - kOff;
+}
+
+// Per-lane masks of a lane's top chunk from round_meta(): w_j <- (w_j & am_j) ^ xm_j keeps
+// the packet's own bytes and injects the initial register (mask_top); the identity for lanes
+// whose top chunk lies wholly inside the packet.
+struct TopMasks {
+  uint32_t am0, am1, am2, am3, xm0, xm1, xm2, xm3;
+};
+__device__ __forceinline__ TopMasks top_masks(uint32_t meta) {
+  const uint32_t head = meta & kMetaHeadMask;
+  const uint32_t v = (meta >> kMetaVShift) & 3u;
+  const uint32_t keep = 0xFFFFFFFFu << (8u * v), kk = head_k(v);
+  const int32_t j0 = head ? 4 - (int32_t)head : -1;  // word index of the top word (-1: no mask)
+  TopMasks m;
+  m.am0 = j0 > 0 ? 0u : (j0 == 0 ? keep : 0xFFFFFFFFu);
+  m.am1 = j0 > 1 ? 0u : (j0 == 1 ? keep : 0xFFFFFFFFu);
+  m.am2 = j0 > 2 ? 0u : (j0 == 2 ? keep : 0xFFFFFFFFu);
+  m.am3 = j0 == 3 ? keep : 0xFFFFFFFFu;
+  m.xm0 = j0 == 0 ? kk : 0u;
+  m.xm1 = j0 == 1 ? kk : 0u;
+  m.xm2 = j0 == 2 ? kk : 0u;
+  m.xm3 = j0 == 3 ? kk : 0u;
+  return m;
+}
+__device__ __forceinline__ uint32_t and_xor(uint32_t w, uint32_t a, uint32_t x) {
+  return (w & a) ^ x;  // one v_bitop3
+}
+
+// A fast round: NS unrolled slots.  Lane tops lie in slots B..B + spread (all < the ring,
+// so the previous round issued their DMAs with per-lane sources: the zero chunk before a
+// lane's top); each lane masks its own top chunk there.  Slot B starts the streams without
+// lookups (a stream is zero before its lane's top).  Slots before B (NS == ring) are only
+// consumed.
+template <int S, int NS, int B>
+__device__ __forceinline__ void round16_slot(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
+                                             const LaneConsts& c, const TopMasks& m, uint32_t& h0, uint32_t& h1,
+                                             uint32_t& h2, uint32_t& h3) {
+  constexpr int kF = S + kRaggedRing;  // refill this slot's position kRaggedRing slots ahead
+  const u32x4 v = R.nextv;
+  if constexpr (kF < NS)
+    dma16<kStep4 * (uint32_t)kF>(cur.cb, R.at<S>());
+  else
+    dma16<kStep4 * (uint32_t)(kF - NS)>(ragged16_base<kStep4 * (uint32_t)(kF - NS)>(nxt, kF - NS, c.dummy), R.at<S>());
+  const uint32_t next_addr = R.at<S + 1>() + R.lane16;
+  if constexpr (S < B) {
+    R.nextv = read_landed_slot<kRaggedRing - 1>(next_addr);
+  } else {
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    if constexpr (S == NS - 1) w3 &= cur.last_mask;  // data only: before the injection
+    if constexpr (S < kRaggedRing) {
+      if (NS == kRaggedRing || S - B <= cur.spread) {
+        if (cur.top_slot == S) {
+          w0 = and_xor(w0, m.am0, m.xm0);
+          w1 = and_xor(w1, m.am1, m.xm1);
+          w2 = and_xor(w2, m.am2, m.xm2);
+          w3 = and_xor(w3, m.am3, m.xm3);
+        }
+      }
+    }
+    if constexpr (S == B) {
+      h0 = w0;  // M32^16(0) = 0: no lookups
+      h1 = w1;
+      h2 = w2;
+      h3 = w3;
+      R.nextv = read_landed_slot<kRaggedRing - 1>(next_addr);
+    } else {
+      horner_step_and_read<kRaggedRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
+    }
+  }
+  issue_order_fence();
+}
+
+template <int NS, int B, int... S>
+__device__ __forceinline__ void round16_slots(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
+                                              const LaneConsts& c, const TopMasks& m, uint32_t& h0, uint32_t& h1,
+                                              uint32_t& h2, uint32_t& h3, std::integer_sequence<int, S...>) {
+  (round16_slot<S, NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3), ...);
+}
+
+template <int NS, int B>
+__device__ __forceinline__ void round16_fast(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
+                                             const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                             uint32_t& h3) {
+  static_assert(B == 0 || NS == kRaggedRing, "leading consumed slots only in ring-length rounds");
+  const TopMasks m = top_masks(cur.meta);
+  round16_slots<NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3, std::make_integer_sequence<int, NS>{});
+  R.rotate((uint32_t)(NS % 3));
+}
+
+// Any round (wider spreads, longer packets, chunks below the caller's buffer): per-lane top
+// slot, runtime slot count.
+__device__ __forceinline__ void round16_generic(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
+                                                const LaneConsts& c, const uint32_t* lds, uint32_t& h0,
+                                                uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  uint32_t m = 0;  // s % 3
+  for (int32_t s = 0; s < cur.ns; ++s) {
+    const u32x4 v = R.nextv;
+    const int32_t f = s + kRaggedRing;
+    const uint64_t src = f < cur.ns ? ragged_src<kStep4>(cur, f, c.dummy) : ragged_src<kStep4>(nxt, f - cur.ns, c.dummy);
+    dma16(src, R.at_rt(m));
+    m = m == 2u ? 0u : m + 1u;
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    const bool top = s == cur.top_slot;
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
+      if (top && (cur.meta & kMetaFallback))
+        load_top_words(cur.cb + (uint64_t)kStep4 * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
+    }
+    if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
+    }
+    h0 = horner_main(lds, h0, w0, c.lk);
+    h1 = horner_main(lds, h1, w1, c.lk);
+    h2 = horner_main(lds, h2, w2, c.lk);
+    h3 = horner_main(lds, h3, w3, c.lk);
+    R.nextv = read_landed_slot<kRaggedRing - 1>(R.at_rt(m) + R.lane16);
+    issue_order_fence();
+  }
+  R.rotate(m);
+}
+
+template <int... I>
+__device__ __forceinline__ bool round16_dispatch(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
+                                                 const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                                 uint32_t& h3, std::integer_sequence<int, I...>) {
+  if (cur.ns == kRaggedRing) {
+    if (cur.top_uniform == 0) round16_fast<kRaggedRing, 0>(cur, nxt, R, c, h0, h1, h2, h3);
+    else if (cur.top_uniform == 1) round16_fast<kRaggedRing, 1>(cur, nxt, R, c, h0, h1, h2, h3);
+    else if (cur.top_uniform == 2) round16_fast<kRaggedRing, 2>(cur, nxt, R, c, h0, h1, h2, h3);
+    else return false;
+    return true;
+  }
+  return ((cur.ns == I + kRaggedRing + 1 ? (round16_fast<I + kRaggedRing + 1, 0>(cur, nxt, R, c, h0, h1, h2, h3), true)
+                                         : false) ||
+          ...);
+}
+
+// The 4 word streams of each of the group's 4 lanes combined into y (register = M32 y),
+// valid on lane k == 0: in-lane Horner with M32^1 (replicated, conflict-free), then the
+// 2-level tree M32^4, M32^8 (unreplicated; only the lanes whose value moves look up).
+__device__ __forceinline__ uint32_t combine_tree4(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
+                                                  uint32_t h3, const Lookup& lk) {
+  uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
+  y = apply_rep(lds, y, h2, lk.lp1, lk);
+  y = apply_rep(lds, y, h3, lk.lp1, lk);
+  const uint32_t k = threadIdx.x & (kG4 - 1);
+  uint32_t t = 0;
+  if (k & 1u) t = apply_small(lds + kRepDwords, y);
+  y ^= from_lane_plus<1>(t);
+  if (k == 2u) t = apply_small(lds + kRepDwords + 1024, y);
+  y ^= from_lane_plus<2>(t);
+  return y;
+}
+
+__device__ __forceinline__ void lds_st8_nowait(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b8 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
+  asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
+  send_servers_home();
+  constexpr int kDmaRing = kRaggedRing;
+  __shared__ __attribute__((aligned(16))) Ragged16Lds S;
+  uint32_t* const lds = S.tables;
+  constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
+  if (threadIdx.x < (unsigned)kJobSlots4) {
+    S.ready[threadIdx.x] = 0;
+    S.consumed[threadIdx.x] = 0;
+    S.done[threadIdx.x] = 0;
+    S.freed[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) {
+    S.next_dispatch = kWavesPerBlock * kLook;
+    S.failed = 0;
+  }
+  fill_lds4(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(b.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t k4 = lane & (kG4 - 1), g4 = lane / kG4;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
+
+  auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
+  const uint32_t JP = b.job_packets;
+  auto job_count = [&](uint64_t J) -> uint32_t {  // packets in job J (J < njobs)
+    const uint64_t left = b.count - J * JP;
+    return left < (uint64_t)JP ? (uint32_t)left : JP;
+  };
+  // Round d of this workgroup: round d % RJ of its (d / RJ)-th job (d / RJ as one s_mul_hi,
+  // exact below 2^27 rounds: launch_ragged checks).
+  const uint32_t RJ = JP / kPW4;
+  const uint32_t rj_magic = 0xFFFFFFFFu / RJ + 1u;
+  auto div_rj = [&](uint32_t x) -> uint32_t { return __umulhi(x, rj_magic); };
+  auto round_valid = [&](uint32_t d) -> bool {
+    const uint32_t k = div_rj(d);
+    const uint64_t J = job_of(k);
+    return J < b.njobs && (uint64_t)(d - k * RJ) * kPW4 < job_count(J);
+  };
+
+  // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
+  // u32 lengths at +4096): six 16-B DMAs per lane, or, near the batch end, 24 4-B DMAs
+  // clamped to the batch.
+  auto job_dma = [&](uint64_t J, uint32_t slot) {
+    LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
+    const uint64_t p0 = J * JP;
+    if (p0 + kJobPackets4 <= b.count) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 * i + 2 * lane), (LdsVoid*)(st + 1024 * i),
+                                         16, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 256 * i + 4 * lane),
+                                         (LdsVoid*)(st + 4096 + 1024 * i), 16, 0, 0);
+    } else {
+      // Not unrolled: one address live at a time (see crc32_ragged_jobs_kernel).
+      const uint32_t* offw = reinterpret_cast<const uint32_t*>(b.offsets);
+#pragma unroll 1
+      for (uint32_t i = 0; i < 24; ++i) {
+        const uint32_t w = 64u * (i & 15u) + lane;
+        const uint64_t e = i < 16 ? p0 + w / 2 : p0 + 64u * (i - 16u) + lane;
+        const void* src = e >= b.count ? (const void*)g_zero_chunk
+                          : i < 16   ? (const void*)(offw + 2 * e + (w & 1u))
+                                     : (const void*)(b.lengths + e);
+        __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 256 * i), 4, 0, 0);
+      }
+    }
+  };
+  // Phase B (>= kDmaRing DMAs after phase A): sort the job's packets by step class, write
+  // its round records and headers in place of the descriptors, then mark the slot ready.
+  // The sort is a histogram in LDS: each packet's ds_add_rtn on its class counter returns
+  // its rank in the class (in some lane order; results go out by local id, so any order
+  // is right), one wave scan turns the counts into first positions.
+  auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
+    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDmaRing - 1) : "memory");
+    const uint32_t st = lds_addr(&S.job[slot].rec[0]);
+    const uint32_t hd = lds_addr(&S.job[slot].head[0]);
+    const uint32_t hi = lds_addr(&S.job[slot].hist[0]);
+    const uint32_t n = job_count(J);
+    // Lane id from an asm statement: the compiler cannot hoist the per-packet local ids
+    // out of the round loop (hoisted, they were spilled to scratch).
+    uint32_t ln8;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 3, %0"
+                 : "=v"(ln8));
+    if (lane < 32u) {
+      lds_st32_nowait(hi + 4u * lane, 0u);
+      lds_st32_nowait(hd + 4u * lane, 0u);
+    }
+    uint64_t ax[8];
+    uint32_t info[8], cls[8], pos[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // 4 packets at a time: 8B offsets at 8 id, lengths at 4096 + 4 id
+      const u32x4 o01 = lds_ld128(st + 8u * ln8 + 32u * h), o23 = lds_ld128(st + 8u * ln8 + 32u * h + 16u);
+      const u32x4 ll = lds_ld128(st + 4096u + 4u * ln8 + 16u * h);
+      const uint64_t off[4] = {o01.x | (uint64_t)o01.y << 32, o01.z | (uint64_t)o01.w << 32,
+                               o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
+      const uint32_t len[4] = {ll.x, ll.y, ll.z, ll.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * h + j;
+        const uint32_t id = ln8 + (uint32_t)i;
+        const bool v = id < n;
+        const RaggedRecord rec = ragged_record4(b.base + off[j], len[j], c.base4);
+        ax[i] = v ? rec.ax | ((uint64_t)id << kJobLidShift4) : 0ull;
+        info[i] = rec.info;
+        // Longer packets and chunks that may reach below the caller's buffer sort last,
+        // in the class whose rounds take the generic body.
+        const bool lng = rec.nsteps >= kClassLong4 || ((rec.ax >> kRecNearBit) & 1u);
+        cls[i] = !v ? kClassNone4 : (lng ? kClassLong4 : rec.nsteps);
+      }
+    }
+    // Ranks in the class (the adds follow the zeroing above: one wave, LDS in order).
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pos[i] = lds_add_rtn(hi + 4u * cls[i], 1u);
+    uint32_t cnt = 0;  // counts -> first positions (exclusive scan over the classes, whole wave)
+    if (lane < 32u) cnt = lds_ld32(hi + 4u * lane);
+    const uint32_t first = wave_inclusive_add(cnt) - cnt;
+    if (lane < 32u) lds_st32(hi + 4u * lane, first);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t q = lds_ld32(hi + 4u * cls[i]) + pos[i];
+      const uint32_t r = st + (q >> 4) * kRound4Bytes;
+      lds_st64(r + 8u * (q & 15u), ax[i]);
+      lds_st32(r + 128u + 4u * (q & 15u), info[i]);
+      if (cls[i] != kClassNone4) {
+        const uint32_t h = hd + 4u * (q >> 4);
+        const uint32_t ns8 = min(info[i] & kRecStepsMask, 255u);
+        if ((q & 15u) == 0u) lds_st8_nowait(h, ns8);
+        if ((q & 15u) == 15u || q + 1u == n) lds_st8_nowait(h + 1u, ns8);
+        if (cls[i] == kClassLong4) lds_or_nowait(h, kHeadGeneric);
+      }
+    }
+    if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);  // waits for every LDS write above
+  };
+
+  // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
+  // (rounds 0 .. 2 x 16 - 1) and kJobAhead4 more.  RJ >= 16 (launch_ragged), so that is at
+  // most 2 + kJobAhead4 = kJobSlots4 jobs.
+  const uint32_t first_jobs = (kWavesPerBlock * kLook - 1) / RJ + kJobAhead4 + 1;
+  if (wv < first_jobs && job_of(wv) < b.njobs) {
+    job_dma(job_of(wv), wv);
+    __builtin_amdgcn_s_waitcnt(0);
+    job_build(job_of(wv), wv, wv + 1u);
+  }
+  __syncthreads();
+
+  uint32_t seen_ready = 0, seen_freed = 0;
+  const uint32_t fail_a = lds_addr(&S.failed);
+  auto waited = [&](uint32_t w, uint32_t bit) -> bool {
+    if (w == kWaitGaveUp) report_fault(fail_a, bit);
+    return w == kWaitOk;
+  };
+  auto make_round = [&](uint32_t d) -> RaggedRound {
+    uint64_t ax = 0;
+    uint32_t info = 0, hdr = 0;
+    const uint32_t k = div_rj(d), slot = k & (uint32_t)(kJobSlots4 - 1), rj = d - k * RJ;
+    const uint64_t J = job_of(k);
+    const uint32_t n = J < b.njobs ? job_count(J) : 0u;
+    const bool live = rj * kPW4 < n;  // round_valid(d)
+    bool rv = live;
+    if (rv && k + 1u > seen_ready) {
+      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
+      if (rv) seen_ready = k + 1u;
+    }
+#ifdef ENET_CRC_TEST_HOOKS
+    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k) rv = waited(kWaitGaveUp, kFaultReady);
+#endif
+    if (rv) {
+      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + rj * kRound4Bytes;
+      asm volatile("ds_read_b64 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(ax), "=&v"(info), "=&v"(hdr)
+                   : "v"(r + 8u * g4), "v"(r + 128u + 4u * g4), "v"(lds_addr(&S.job[slot].head[rj]))
+                   : "memory");
+      hdr = __builtin_amdgcn_readfirstlane(hdr);
+      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
+    }
+    RaggedRound rr = round16_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), hdr, c);
+    rr.live = live;
+    rr.job_k = k;
+    rr.job_rounds = (n + kPW4 - 1) / kPW4;
+    return rr;
+  };
+
+  uint32_t rnd0 = wv, rnd1 = wv + kWavesPerBlock;
+  if (!round_valid(rnd0)) return;
+  RaggedRound cur = make_round(rnd0);
+  RaggedRound nxt = make_round(rnd1);
+  Ring3 R;
+  R.a0 = lds_addr(&S.ring[0][wv][0]);
+  R.a1 = lds_addr(&S.ring[1][wv][0]);
+  R.a2 = lds_addr(&S.ring[2][wv][0]);
+  R.lane16 = lane * 16u;
+  dma16(ragged_src<kStep4>(cur, 0, c.dummy), R.a0);  // cur.ns >= kDmaRing
+  dma16(ragged_src<kStep4>(cur, 1, c.dummy), R.a1);
+  dma16(ragged_src<kStep4>(cur, 2, c.dummy), R.a2);
+  R.nextv = read_landed_slot<kDmaRing - 1>(R.a0 + R.lane16);
+  while (cur.live) {  // cur is round rnd0
+    uint32_t d = 0;
+    if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
+    d = __builtin_amdgcn_readfirstlane(d);
+    // Build duty: the claimer of a job's first round builds the job kJobAhead4 later once
+    // every round of the slot's previous job has read its record (crc32_ragged_jobs_kernel).
+    bool build = false;
+    const uint32_t kd = div_rj(d), kb = kd + kJobAhead4, bslot = kb & (uint32_t)(kJobSlots4 - 1);
+    if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
+      build = kb < (uint32_t)kJobSlots4 ||
+              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
+      if (build) {
+        if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
+        job_dma(job_of(kb), bslot);
+      }
+    }
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    if (!cur.fast || !round16_dispatch(cur, nxt, R, c, h0, h1, h2, h3,
+                                       std::make_integer_sequence<int, kFast4Max - kRaggedRing>{}))
+      round16_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
+    const uint32_t y = combine_tree4(lds, h0, h1, h2, h3, c.lk);
+    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k4 == 0 holds it
+    if (cur.meta & kMetaEmpty) reg = kInitRegister;
+    // The round's checksums into the job's result array; the last round of a job writes
+    // the job's checksums to HBM.
+    const uint32_t k0 = cur.job_k, slot0 = k0 & (uint32_t)(kJobSlots4 - 1);
+    if (k0 >= (uint32_t)kJobSlots4 && k0 + 1u - (uint32_t)kJobSlots4 > seen_freed) {
+      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots4 + 1u, fail_a), kFaultFreed))
+        seen_freed = k0 + 1u - (uint32_t)kJobSlots4;
+    }
+    if (k4 == 0 && (cur.meta & kMetaStore))
+      lds_st32_nowait(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
+    uint32_t old = 0;
+    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old + 1u == cur.job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
+      const uint64_t J0 = job_of(k0);
+      const uint32_t n0 = job_count(J0);
+      const uint32_t ra = lds_addr(&S.job[slot0].res[0]) + 32u * lane;
+      u32x4 v0, v1;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(v0), "=&v"(v1)
+                   : "v"(ra), "v"(ra + 16u)
+                   : "memory");
+      uint32_t* dst = out + J0 * JP + 8u * lane;
+      if (8u * lane + 8u <= n0) {
+        reinterpret_cast<U32x4A4*>(dst)->v = v0;
+        reinterpret_cast<U32x4A4*>(dst + 4)->v = v1;
+      } else {
+        const uint32_t e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+          if (8u * lane + (uint32_t)i < n0) dst[i] = e[i];
+      }
+    }
+    if (old + 1u == cur.job_rounds && lane == 0) {
+      lds_st32(lds_addr(&S.done[slot0]), 0u);
+      lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
+    }
+    if (build) job_build(job_of(kb), bslot, kb + 1u);
+    const RaggedRound after = make_round(d);
+    rnd0 = rnd1;
+    rnd1 = d;
+    cur = nxt;
+    nxt = after;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
 }  // namespace
 
 int cu_count_for_current_device();
@@ -2212,16 +2803,21 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.  Workgroups
-  // take jobs statically, so the launch lasts as long as the busiest workgroup's
-  // ceil(njobs / grid) jobs: the job size (16..32 rounds of 8 packets) is the one that
-  // minimises that makespan in rounds (1M packets on 256 CUs: 32 rounds, 16 jobs each;
-  // on 248 CUs: 23 rounds, 23 jobs each instead of 17 or 16 jobs of 32).
+  // In-kernel job sort (crc32_ragged16_kernel; crc32_ragged_jobs_kernel in the
+  // ENET_CRC_RAGGED8 A/B build): one launch, no scratch.  Workgroups take jobs statically,
+  // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
+  // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
+  // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
+#ifdef ENET_CRC_RAGGED8
+  constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds;
+#else
+  constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRounds4;
+#endif
   const int cus = cu_count_for_current_device();
   if (cus <= 0) return hipErrorNoDevice;
-  uint64_t jp = kJobPackets, njobs = 0, best = ~0ull;
-  for (uint64_t rj = kJobRounds; rj >= kJobRounds / 2; --rj) {
-    const uint64_t p = rj * kPacketsPerWave, nj = (count + p - 1) / p;
+  uint64_t jp = kMaxJobRounds * kRoundPackets, njobs = 0, best = ~0ull;
+  for (uint64_t rj = kMaxJobRounds; rj >= kMaxJobRounds / 2; --rj) {
+    const uint64_t p = rj * kRoundPackets, nj = (count + p - 1) / p;
     const uint64_t grid = nj < (uint64_t)cus ? nj : (uint64_t)cus;
     const uint64_t span = (nj + grid - 1) / grid * rj;
     if (span < best) {
@@ -2234,7 +2830,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   // The kernel divides a workgroup's round index by RJ with one s_mul_hi, exact below 2^27
   // rounds (div_rj); a batch whose busiest workgroup would go past that (a device with few
   // CUs and billions of packets) takes the streaming kernel instead.
-  const uint64_t wg_rounds = (njobs + jblocks - 1) / jblocks * (jp / kPacketsPerWave) + 2 * kWavesPerBlock;
+  const uint64_t wg_rounds = (njobs + jblocks - 1) / jblocks * (jp / kRoundPackets) + 2 * kWavesPerBlock;
   if (wg_rounds >= (1ull << 27)) {
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
@@ -2250,7 +2846,11 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
   jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
 #endif
+#ifdef ENET_CRC_RAGGED8
   hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+#else
+  hipLaunchKernelGGL(crc32_ragged16_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+#endif
   return hipGetLastError();
 }
 

@@ -6,8 +6,8 @@
 // order-2 model that codes the next one), so the parallelism is across packets:
 // one lane = one coder = one packet at a time (grid-stride over the batch).
 // Each lane owns a 64 KiB symbol arena (4096 x 16-B ENetSymbol, compress.rs:7-22)
-// in HBM scratch.  A symbol is read as ONE 16-byte load; updates are narrow
-// stores to the fields that change.  The work is a chain of dependent arena
+// in HBM scratch.  A symbol is read as ONE 16-byte load; updates store whole
+// 32-bit words rebuilt from the loaded copy.  The work is a chain of dependent arena
 // loads (tree walks in up to three contexts per byte), so the kernel is
 // latency-bound, not bandwidth-bound: throughput comes from the number of lanes
 // in flight (the `workers` argument sizes the scratch and the grid).
