@@ -4,7 +4,7 @@
 # status or exit 3 = no box free).  A command that ran and failed is never retried.
 #   scripts/gpurun_retry.sh <timeout-seconds> '<command>'
 T="$1"; shift
-for attempt in 1 2 3 4 5 6; do
+for attempt in $(seq 1 ${GPURUN_ATTEMPTS:-6}); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@"
   rc=$?
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)

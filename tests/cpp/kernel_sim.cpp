@@ -153,10 +153,12 @@ int main() {
     const uint64_t len = it < 6000 ? (uint64_t)(it % 600) : g() % (it % 11 == 0 ? 300000 : 3000);
     if (s + len > buf.size()) continue;
     const uint32_t want = oracle_crc32(buf.data() + s, len);
-    // model<64, true>: the wave-per-packet kernel (crc32_wave_dma_kernel, 1-KiB steps).
-    const uint32_t got[6] = {model<2>(buf.data(), s, len), model<4>(buf.data(), s, len),
+    // model<64, true>: the wave-per-packet kernel (crc32_wave_dma_kernel, 1-KiB steps);
+    // model<4, true>: the 16-packet ragged kernel (crc32_ragged16_kernel, 64-B steps).
+    const uint32_t got[7] = {model<2>(buf.data(), s, len), model<4>(buf.data(), s, len),
                              model<8>(buf.data(), s, len), model<16>(buf.data(), s, len),
-                             model<8, true>(buf.data(), s, len), model<64, true>(buf.data(), s, len)};
+                             model<8, true>(buf.data(), s, len), model<64, true>(buf.data(), s, len),
+                             model<4, true>(buf.data(), s, len)};
     for (uint32_t v : got) {
       if (v != want) {
         if (bad < 10) printf("mismatch s=%llu len=%llu want %08x got %08x\n", (unsigned long long)s,

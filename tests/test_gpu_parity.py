@@ -290,6 +290,43 @@ def test_ragged_region_sort_edges(dev, count):
     assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
 
 
+@pytest.mark.parametrize("shape", ["near_base", "wide_spread", "tiny", "long_mix", "mtu_unaligned", "one_job"])
+def test_ragged16_round_paths(dev, shape):
+    """The round bodies of crc32_ragged16_kernel (16 packets per round, 64-B steps):
+    near_base: overlapping packets starting in the first 16 bytes of the buffer (top chunks
+    that would reach below it: the generic body's fallback loads); wide_spread: six step
+    classes far apart, so the rounds where classes meet differ by > 2 steps (generic body);
+    tiny: packets of <= 3 steps at every alignment (ring-length rounds, first top slot
+    0, 1 or 2); long_mix: packets of 23+ steps (the longer class, generic) next to short
+    ones; mtu_unaligned: 1392-B datagrams from base + 1 (the frag_64k shape); one_job: a
+    batch of one partial job per workgroup."""
+    rng = np.random.default_rng(abs(hash(shape)) % (1 << 32))
+    n = 9000
+    if shape == "near_base":
+        lengths = rng.integers(0, 1500, size=n).astype(np.uint32)
+        offsets = rng.integers(0, 16, size=n).astype(np.uint64)
+        data = splitmix64_bytes(61, 16 + 1500 + 8)
+    else:
+        if shape == "wide_spread":
+            lengths = rng.choice(np.array([40, 300, 560, 820, 1080, 1340], dtype=np.uint32), size=n)
+        elif shape == "tiny":
+            lengths = rng.integers(0, 193, size=n).astype(np.uint32)
+        elif shape == "long_mix":
+            lengths = np.where(rng.random(n) < 0.5, rng.integers(1400, 4097, size=n),
+                               rng.integers(0, 200, size=n)).astype(np.uint32)
+        elif shape == "mtu_unaligned":
+            lengths = np.full(n, 1392, dtype=np.uint32)
+        else:
+            n = 4096 + 17
+            lengths = rng.integers(0, 1500, size=n).astype(np.uint32)
+        gaps = rng.integers(0, 5, size=n).astype(np.uint64) if shape in ("tiny", "long_mix") else np.zeros(n, np.uint64)
+        offsets = (packed_offsets(lengths) + np.cumsum(gaps)).astype(np.uint64) + np.uint64(1)
+        data = splitmix64_bytes(62, int(offsets[-1] + lengths[-1]) + 8)
+    got = ragged_on_device(data, offsets, lengths, dev)
+    want = _oracle.crc32_ragged(data, offsets, lengths)
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+
+
 # --- round-record scratch cached per stream (launch_ragged) ----------------------------------
 
 def test_ragged_scratch_per_stream(dev):
