@@ -29,6 +29,8 @@ pub struct enet_crc_ctx {
 }
 
 pub const ENET_CRC_OK: c_int = 0;
+/// A batch kernel gave up on the device: the call's outputs are invalid (ABI 6).
+pub const ENET_CRC_E_DEVICE: c_int = -5;
 pub const ENET_CRC_PERCALL_COPY: c_int = 0;
 pub const ENET_CRC_PERCALL_ZEROCOPY: c_int = 1;
 pub const ENET_CRC_PERCALL_PERSISTENT: c_int = 2;
@@ -195,6 +197,18 @@ impl GpuCrc32 {
             return Err(last_error(st));
         }
         Ok(())
+    }
+
+    /// The device-side failure word of `device` (ABI 6): `Ok(0)` if no batch kernel gave
+    /// up since the last clear, else the failure bits; check it (with `clear`) after the
+    /// asynchronous device entries before trusting their outputs.  The host entries below
+    /// return `ENET_CRC_E_DEVICE` (-5) instead.
+    pub fn device_status(device: i32, clear: bool) -> Result<i32, CrcError> {
+        let st = unsafe { enet_crc_device_status(device, clear as c_int) };
+        if st < 0 {
+            return Err(last_error(st));
+        }
+        Ok(st)
     }
 
     /// Same contract as `rusty_enet::crc32` (src/crc32.rs:39), but fallible.

@@ -2179,19 +2179,11 @@ struct Ring3 {
   }
 };
 
-// One 16-B LDS-DMA per lane into the ring position at LDS byte address `lds`; kOff is the
-// instruction's immediate offset (no address arithmetic per slot).
-template <uint32_t kOff = 0>
+// One 16-B LDS-DMA per lane from `src` into the ring position at LDS byte address `lds`.
+// (No immediate offset: the instruction applies it to the LDS address as well as to the
+// global one, so a step offset there would land the data past the ring position.)
 __device__ __forceinline__ void dma16(uint64_t src, uint32_t lds) {
-  __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)(uintptr_t)lds, 16, kOff, 0);
-}
-
-// Source of slot f of round rr (64-B steps) as base + kOff: the zero chunk before the lane's
-// top (base = dummy - kOff), its chunk from there on.
-template <uint32_t kOff>
-__device__ __forceinline__ uint64_t ragged16_base(const RaggedRound& rr, int32_t f, uint64_t dummy) {
-  const bool real = f > rr.top_slot || (f == rr.top_slot && (rr.meta & kMetaDirect));
-  return real ? rr.cb : dummy - kOff;
+  __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)(uintptr_t)lds, 16, 0, 0);
 }
 
 // Per-lane masks of a lane's top chunk from round_meta(): w_j <- (w_j & am_j) ^ xm_j keeps
@@ -2232,9 +2224,9 @@ __device__ __forceinline__ void round16_slot(const RaggedRound& cur, const Ragge
   constexpr int kF = S + kRaggedRing;  // refill this slot's position kRaggedRing slots ahead
   const u32x4 v = R.nextv;
   if constexpr (kF < NS)
-    dma16<kStep4 * (uint32_t)kF>(cur.cb, R.at<S>());
+    dma16(cur.cb + (uint64_t)kStep4 * kF, R.at<S>());  // inside every valid packet (kF > its top slot)
   else
-    dma16<kStep4 * (uint32_t)(kF - NS)>(ragged16_base<kStep4 * (uint32_t)(kF - NS)>(nxt, kF - NS, c.dummy), R.at<S>());
+    dma16(ragged_src<kStep4>(nxt, kF - NS, c.dummy), R.at<S>());
   const uint32_t next_addr = R.at<S + 1>() + R.lane16;
   if constexpr (S < B) {
     R.nextv = read_landed_slot<kRaggedRing - 1>(next_addr);
@@ -2484,7 +2476,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16
         const uint32_t ns8 = min(info[i] & kRecStepsMask, 255u);
         if ((q & 15u) == 0u) lds_st8_nowait(h, ns8);
         if ((q & 15u) == 15u || q + 1u == n) lds_st8_nowait(h + 1u, ns8);
-        if (cls[i] == kClassLong4) lds_or_nowait(h, kHeadGeneric);
+        // Longer packets, chunks near the caller's base, and the job's partial last round:
+        // its empty groups' chunk addresses lie below the base, which only the generic
+        // body's per-lane sources keep from being read.
+        if (cls[i] == kClassLong4 || ((q & 15u) != 15u && q + 1u == n)) lds_or_nowait(h, kHeadGeneric);
       }
     }
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);  // waits for every LDS write above
