@@ -659,6 +659,8 @@ def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, bar
            "kernel_ms": round(kms, 5), "frac": round(nbytes / (kms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
     cf = ceiling_fields(ceil, pre, spec[1] if ceil else None, nbytes, nbytes / (kms / 1000.0) / 1e9)
     res["read_ceiling_gbs"], res["frac_of_ceiling"] = cf["read_ceiling_gbs"], cf["frac_of_ceiling"]
+    if name in ("ragged", "large", "frag") and n == CONFIGS[name][1]:
+        res["traffic"] = load_pmc_traffic(name)[0]  # HBM bytes per launch, committed profile, same sources
     del spec, out
     torch.cuda.empty_cache()
     return res

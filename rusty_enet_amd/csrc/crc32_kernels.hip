@@ -1387,15 +1387,26 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
         h2 = w2;
         h3 = w3;
       } else {
+#ifdef ENET_CRC_PROBE_G1_NOLOOKUPS  // measurement build only (wrong checksums): the loads alone
+        h0 ^= w0;
+        h1 ^= w1;
+        h2 ^= w2;
+        h3 ^= w3;
+#else
         h0 = horner_main(lds, h0, w0, c.lk);
         h1 = horner_main(lds, h1, w1, c.lk);
         h2 = horner_main(lds, h2, w2, c.lk);
         h3 = horner_main(lds, h3, w3, c.lk);
+#endif
       }
       issue_order_fence();
       q[s] = ld(lbn, s);  // the next round's slot s
       issue_order_fence();
     }
+#if defined(ENET_CRC_PROBE_G1_NOCOMBINE) || defined(ENET_CRC_PROBE_G1_NOLOOKUPS)
+    // Measurement builds only (wrong checksums): no handover, no combine.
+    const uint32_t reg = h0 ^ h1 ^ h2 ^ h3 ^ (uint32_t)kept.x;
+#else
     {
       const uint32_t a = ll.src4;
       const uint32_t x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.x);
@@ -1411,6 +1422,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
     }
     const uint32_t y = combine_tree_rep(lds, h0, h1, h2, h3, c.lk);
     const uint32_t reg = finish_word(lds, y, 0u, c.lk);
+#endif
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
       res = crc;
@@ -2798,12 +2810,12 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // In-kernel job sort (crc32_ragged16_kernel; crc32_ragged_jobs_kernel in the
-  // ENET_CRC_RAGGED8 A/B build): one launch, no scratch.  Workgroups take jobs statically,
+  // In-kernel job sort (crc32_ragged_jobs_kernel; crc32_ragged16_kernel in the
+  // ENET_CRC_RAGGED16 build until it has been measured on the GPU): one launch, no scratch.  Workgroups take jobs statically,
   // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
   // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
   // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
-#ifdef ENET_CRC_RAGGED8
+#ifndef ENET_CRC_RAGGED16
   constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds;
 #else
   constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRounds4;
@@ -2841,7 +2853,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
   jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
 #endif
-#ifdef ENET_CRC_RAGGED8
+#ifndef ENET_CRC_RAGGED16
   hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
 #else
   hipLaunchKernelGGL(crc32_ragged16_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);

@@ -6,12 +6,12 @@
 set -eu
 SRC="$1"; DST="$2"
 mkdir -p "$DST"
-for c in uniform ragged large range; do
+for c in uniform ragged large frag range; do
   cp "$SRC/bench_$c.json" "$DST/"
   cp "$SRC/prof_$c/run_kernel_stats.csv" "$DST/${c}_kernel_stats.csv"
   python3 scripts/pmc_summary.py "$SRC/pmc_$c" > "$DST/${c}_pmc_summary.txt" 2>&1
 done
-for f in ipc_uniform_summary.txt ipc_ragged_summary.txt traffic.json pytest_gpu.log bench_rehearsal_n2.json; do
+for f in ipc_uniform_summary.txt ipc_ragged_summary.txt ipc_frag_summary.txt traffic.json pytest_gpu.log bench_rehearsal_n2.json; do
   [ -f "$SRC/$f" ] && cp "$SRC/$f" "$DST/"
 done
 cp "$SRC/traffic.json" profiles/pmc_traffic.json

@@ -14,7 +14,7 @@ mkdir -p "$OUT"
 cd "$ROOT"
 timeout -k 10 300 python bench.py > "$OUT/bench_uniform.json" 2> "$OUT/bench_uniform.err" || exit $?
 echo "[profile] uniform bench done" >&2
-for c in ragged large; do
+for c in ragged large frag; do
   timeout -k 10 200 python bench.py --config $c --cpu-seconds 0 --no-e2e > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || exit $?
   echo "[profile] $c bench done" >&2
 done
@@ -22,14 +22,14 @@ timeout -k 10 300 python bench.py --config range > "$OUT/bench_range.json" 2> "$
 echo "[profile] range bench done" >&2
 export TMPDIR=/tmp
 cd /tmp
-for c in uniform ragged large range; do
+for c in uniform ragged large frag range; do
   steps=20; [ $c = range ] && steps=3
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o run --output-format csv \
     -- python3 "$ROOT/bench.py" --config $c --steps $steps --warmup 2 --cpu-seconds 0 --no-verify --no-e2e --no-shard \
     > "$OUT/prof_$c.log" 2>&1 || exit $?
   echo "[profile] $c kernel stats done" >&2
 done
-for c in uniform ragged large; do
+for c in uniform ragged large frag; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_$c" -o run --output-format csv \
     -- python3 "$ROOT/bench.py" --config $c --steps 5 --warmup 1 --cpu-seconds 0 --no-verify --no-e2e --no-shard \
     > "$OUT/pmc_$c.log" 2>&1 || exit $?
@@ -44,7 +44,7 @@ for counters in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST
                 "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  for c in uniform ragged; do
+  for c in uniform ragged frag; do
     timeout -k 10 120 rocprofv3 --kernel-trace --pmc $counters -d "$OUT/ipc_${c}_$i" -o run --output-format csv \
       -- python3 "$ROOT/bench.py" --config $c --steps 5 --warmup 1 --cpu-seconds 0 --no-verify --no-e2e --no-shard \
       > "$OUT/ipc_${c}_$i.log" 2>&1 || exit $?
@@ -53,7 +53,15 @@ for counters in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST
 done
 cd "$ROOT"
 python3 scripts/traffic_summary.py "gpurun_out/$TAG" > "$OUT/traffic.json" 2>&1 || exit $?
-for c in uniform ragged; do
+for c in uniform ragged frag; do
   python3 scripts/pmc_summary.py "$OUT"/ipc_${c}_* > "$OUT/ipc_${c}_summary.txt" 2>&1
 done
+# One bench process's per-launch kernel trace, the driver's command shape and the default
+# (the launch-time series behind the line).
+for spec in "20 5" "200 10"; do
+  set -- $spec
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_$1_$2" -o run \
+    -- python3 "$ROOT/bench.py" --steps $1 --warmup $2 --cpu-seconds 0 --no-e2e --no-shard > "$OUT/trace_$1_$2.json" 2> "$OUT/trace_$1_$2.err") || exit $?
+done
+echo "[profile] launch traces done" >&2
 echo "[profile] done" >&2

@@ -21,7 +21,7 @@ from bench import kernel_source_hash  # noqa: E402
 root = sys.argv[1]
 src_hash = kernel_source_hash()
 out = {}
-for cfg in ("uniform", "ragged", "large"):
+for cfg in ("uniform", "ragged", "large", "frag"):
     fetch, dur = {}, {}
     for path in glob.glob(os.path.join(root, f"pmc_{cfg}", "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
