@@ -2810,12 +2810,12 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // In-kernel job sort (crc32_ragged16_kernel; round 3's crc32_ragged_jobs_kernel in the
-  // ENET_CRC_RAGGED8 A/B build): one launch, no scratch.  Workgroups take jobs statically,
+  // In-kernel job sort (crc32_ragged_jobs_kernel; the 16-packet-round crc32_ragged16_kernel
+  // in the ENET_CRC_RAGGED16 measurement build: slower): one launch, no scratch.  Workgroups take jobs statically,
   // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
   // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
   // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
-#ifdef ENET_CRC_RAGGED8
+#ifndef ENET_CRC_RAGGED16
   constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds;
 #else
   constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRounds4;
@@ -2853,7 +2853,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
   jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
 #endif
-#ifdef ENET_CRC_RAGGED8
+#ifndef ENET_CRC_RAGGED16
   hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
 #else
   hipLaunchKernelGGL(crc32_ragged16_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: the GPU suite on the product (16-packet ragged kernel by default), the driver's
+# Round 4: the GPU suite on the product (ragged kernels of both builds), the driver's
 # bench command and the default bench, instruction counters of both ragged builds.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -14,7 +14,7 @@ python scripts/line_summary.py $O/bench_20_5.json
 timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit $?
 python scripts/line_summary.py $O/bench_default.json
 export TMPDIR=/tmp
-for lib in $P $V/libenet_crc_amd_ragged8.so; do
+for lib in $P $V/libenet_crc_amd_ragged16.so; do
   name=$(basename $lib .so)
   for cfg in ragged frag; do
     (cd /tmp && ENET_CRC_AMD_LIB=$GRAFT_REPO_ROOT/$lib timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
