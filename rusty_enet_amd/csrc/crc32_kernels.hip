@@ -2046,8 +2046,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 
 
 // ---------------------------------------------------------------------------------
-// Ragged kernel with rounds of 16 packets, 4 lanes per packet (the default ragged path
-// since round 4).  Same pipeline as crc32_ragged_jobs_kernel above (jobs sorted by step
+// Ragged kernel with rounds of 16 packets, 4 lanes per packet (ENET_CRC_RAGGED16 measurement
+// build: slower than the 8-lane kernel).  Same pipeline as crc32_ragged_jobs_kernel above (jobs sorted by step
 // class in LDS, the LDS-DMA ring, dynamic round dispatch inside the workgroup, results
 // flushed per job, the failure channel), but a group of FOUR lanes owns a packet and a
 // slot covers 64 B of it: a round carries twice the bytes for the same per-round work
@@ -2084,7 +2084,7 @@ constexpr uint32_t kHeadGeneric = 1u << 16;              // round header bit: ge
 constexpr int kJobLidShift4 = 54;                        // local id (0..511) in ax bits 54..62
 static_assert(kRec4Bytes == kJobPackets4 * 12, "staging: u64 offsets + u32 lengths");
 static_assert((kJobSlots4 & (kJobSlots4 - 1)) == 0, "slot = job & (slots - 1)");
-static_assert(kRaggedRing == 3, "top slots 0..2 are issued by the previous round");
+constexpr int kRing16 = 3;  // ring slots per wave (Ring3; top slots 0..2 are issued by the previous round)
 
 struct JobSlot4 {
   u32x4 rec[kRec4Bytes / 16];
@@ -2094,7 +2094,7 @@ struct JobSlot4 {
 };
 struct Ragged16Lds {
   uint32_t tables[kRepDwords + 2 * 1024];  // replicated M32^16 | M32^1 block, then M32^4 and M32^8
-  u32x4 ring[kRaggedRing][kWavesPerBlock][64];
+  u32x4 ring[kRing16][kWavesPerBlock][64];
   JobSlot4 job[kJobSlots4];
   uint32_t ready[kJobSlots4];     // k + 1 once the workgroup's k-th job has its records here
   uint32_t consumed[kJobSlots4];  // rounds of the slot's job whose records have been read
@@ -2147,7 +2147,7 @@ __device__ __forceinline__ RaggedRound round16_from_record(uint64_t ax, uint32_t
     for (int g = 1; g < kPW4; ++g) mx = max(mx, __builtin_amdgcn_readlane(nsteps, g * kG4));
   }
   RaggedRound rr;
-  rr.ns = max(kRaggedRing, mx);
+  rr.ns = max(kRing16, mx);
   rr.cb = a1 - 16u * (uint64_t)(k + 1u) - (uint64_t)kStep4 * (uint64_t)(rr.ns - 1);
   rr.top_slot = rr.ns - nsteps;
   // This lane's chunk at the top step, relative to top: 4 nwords - 16 (k + 4 (nsteps - 1) + 1)
@@ -2166,7 +2166,7 @@ __device__ __forceinline__ RaggedRound round16_from_record(uint64_t ax, uint32_t
   rr.id = (uint32_t)(ax >> kJobLidShift4) & (uint32_t)(kJobPackets4 - 1);
   rr.top_uniform = rr.ns - nsmax;  // B: the first top slot of a fast round
   rr.spread = nsmax - nsmin;
-  rr.fast = !generic && rr.ns <= kFast4Max && (rr.ns == kRaggedRing || rr.spread <= 2);
+  rr.fast = !generic && rr.ns <= kFast4Max && (rr.ns == kRing16 || rr.spread <= 2);
   return rr;
 }
 
@@ -2233,7 +2233,7 @@ template <int S, int NS, int B>
 __device__ __forceinline__ void round16_slot(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
                                              const LaneConsts& c, const TopMasks& m, uint32_t& h0, uint32_t& h1,
                                              uint32_t& h2, uint32_t& h3) {
-  constexpr int kF = S + kRaggedRing;  // refill this slot's position kRaggedRing slots ahead
+  constexpr int kF = S + kRing16;  // refill this slot's position kRing16 slots ahead
   const u32x4 v = R.nextv;
   if constexpr (kF < NS)
     dma16(cur.cb + (uint64_t)kStep4 * kF, R.at<S>());  // inside every valid packet (kF > its top slot)
@@ -2241,12 +2241,12 @@ __device__ __forceinline__ void round16_slot(const RaggedRound& cur, const Ragge
     dma16(ragged_src<kStep4>(nxt, kF - NS, c.dummy), R.at<S>());
   const uint32_t next_addr = R.at<S + 1>() + R.lane16;
   if constexpr (S < B) {
-    R.nextv = read_landed_slot<kRaggedRing - 1>(next_addr);
+    R.nextv = read_landed_slot<kRing16 - 1>(next_addr);
   } else {
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     if constexpr (S == NS - 1) w3 &= cur.last_mask;  // data only: before the injection
-    if constexpr (S < kRaggedRing) {
-      if (NS == kRaggedRing || S - B <= cur.spread) {
+    if constexpr (S < kRing16) {
+      if (NS == kRing16 || S - B <= cur.spread) {
         if (cur.top_slot == S) {
           w0 = and_xor(w0, m.am0, m.xm0);
           w1 = and_xor(w1, m.am1, m.xm1);
@@ -2260,9 +2260,9 @@ __device__ __forceinline__ void round16_slot(const RaggedRound& cur, const Ragge
       h1 = w1;
       h2 = w2;
       h3 = w3;
-      R.nextv = read_landed_slot<kRaggedRing - 1>(next_addr);
+      R.nextv = read_landed_slot<kRing16 - 1>(next_addr);
     } else {
-      horner_step_and_read<kRaggedRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
+      horner_step_and_read<kRing16 - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
     }
   }
   issue_order_fence();
@@ -2279,7 +2279,7 @@ template <int NS, int B>
 __device__ __forceinline__ void round16_fast(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
                                              const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
                                              uint32_t& h3) {
-  static_assert(B == 0 || NS == kRaggedRing, "leading consumed slots only in ring-length rounds");
+  static_assert(B == 0 || NS == kRing16, "leading consumed slots only in ring-length rounds");
   const TopMasks m = top_masks(cur.meta);
   round16_slots<NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3, std::make_integer_sequence<int, NS>{});
   R.rotate((uint32_t)(NS % 3));
@@ -2293,7 +2293,7 @@ __device__ __forceinline__ void round16_generic(const RaggedRound& cur, const Ra
   uint32_t m = 0;  // s % 3
   for (int32_t s = 0; s < cur.ns; ++s) {
     const u32x4 v = R.nextv;
-    const int32_t f = s + kRaggedRing;
+    const int32_t f = s + kRing16;
     const uint64_t src = f < cur.ns ? ragged_src<kStep4>(cur, f, c.dummy) : ragged_src<kStep4>(nxt, f - cur.ns, c.dummy);
     dma16(src, R.at_rt(m));
     m = m == 2u ? 0u : m + 1u;
@@ -2311,7 +2311,7 @@ __device__ __forceinline__ void round16_generic(const RaggedRound& cur, const Ra
     h1 = horner_main(lds, h1, w1, c.lk);
     h2 = horner_main(lds, h2, w2, c.lk);
     h3 = horner_main(lds, h3, w3, c.lk);
-    R.nextv = read_landed_slot<kRaggedRing - 1>(R.at_rt(m) + R.lane16);
+    R.nextv = read_landed_slot<kRing16 - 1>(R.at_rt(m) + R.lane16);
     issue_order_fence();
   }
   R.rotate(m);
@@ -2321,14 +2321,14 @@ template <int... I>
 __device__ __forceinline__ bool round16_dispatch(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
                                                  const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
                                                  uint32_t& h3, std::integer_sequence<int, I...>) {
-  if (cur.ns == kRaggedRing) {
-    if (cur.top_uniform == 0) round16_fast<kRaggedRing, 0>(cur, nxt, R, c, h0, h1, h2, h3);
-    else if (cur.top_uniform == 1) round16_fast<kRaggedRing, 1>(cur, nxt, R, c, h0, h1, h2, h3);
-    else if (cur.top_uniform == 2) round16_fast<kRaggedRing, 2>(cur, nxt, R, c, h0, h1, h2, h3);
+  if (cur.ns == kRing16) {
+    if (cur.top_uniform == 0) round16_fast<kRing16, 0>(cur, nxt, R, c, h0, h1, h2, h3);
+    else if (cur.top_uniform == 1) round16_fast<kRing16, 1>(cur, nxt, R, c, h0, h1, h2, h3);
+    else if (cur.top_uniform == 2) round16_fast<kRing16, 2>(cur, nxt, R, c, h0, h1, h2, h3);
     else return false;
     return true;
   }
-  return ((cur.ns == I + kRaggedRing + 1 ? (round16_fast<I + kRaggedRing + 1, 0>(cur, nxt, R, c, h0, h1, h2, h3), true)
+  return ((cur.ns == I + kRing16 + 1 ? (round16_fast<I + kRing16 + 1, 0>(cur, nxt, R, c, h0, h1, h2, h3), true)
                                          : false) ||
           ...);
 }
@@ -2359,7 +2359,7 @@ __device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
 
 __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
   send_servers_home();
-  constexpr int kDmaRing = kRaggedRing;
+  constexpr int kDmaRing = kRing16;
   __shared__ __attribute__((aligned(16))) Ragged16Lds S;
   uint32_t* const lds = S.tables;
   constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
@@ -2576,7 +2576,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16
     }
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     if (!cur.fast || !round16_dispatch(cur, nxt, R, c, h0, h1, h2, h3,
-                                       std::make_integer_sequence<int, kFast4Max - kRaggedRing>{}))
+                                       std::make_integer_sequence<int, kFast4Max - kRing16>{}))
       round16_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
     const uint32_t y = combine_tree4(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k4 == 0 holds it
@@ -2621,6 +2621,621 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16
     const RaggedRound after = make_round(d);
     rnd0 = rnd1;
     rnd1 = d;
+    cur = nxt;
+    nxt = after;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+// ---------------------------------------------------------------------------------
+// Ragged kernel with 16-packet rounds loaded as 128-B pieces (crc32_ragged16w_kernel).
+// The 16-packet kernel above halves the per-round work per byte, but its DMAs move 64-B
+// pieces of 16 packets and stream slower than the 8-lane kernel's 128-B pieces of 8
+// (DESIGN.md §4).  Here the two are split: a slot is loaded the 8-lane way -- two LDS-DMA
+// instructions, instruction i's lane 8j + k reading chunk k of packet 8i + j's 128-B piece
+// -- and computed the 4-lane way: lane 4p + k reads chunks k + 4 and k of packet p's piece
+// from LDS and runs two Horner steps (M32^16) per slot, streams and combine exactly as in
+// the 16-packet kernel.  A slot is 2 KiB per wave, the ring 2 slots deep (64 KiB per CU in
+// flight); jobs of 256 packets (16 rounds) sorted by 128-B step count with round headers;
+// unrolled bodies for rounds of <= 13 slots whose step counts differ by <= 1.
+// ---------------------------------------------------------------------------------
+constexpr int kRingW = 2;                                  // ring slots per wave (2 KiB each)
+constexpr int kJobPacketsW = 256;                          // 4 per lane of the building wave
+constexpr int kJobRoundsW = kJobPacketsW / kPW4;           // 16
+constexpr int kJobSlotsW = 4;                              // job slots in LDS
+constexpr int kJobAheadW = 2;                              // jobs built ahead of the one claimed
+constexpr uint32_t kRoundWBytes = 192;                     // per round: u64 ax[16], u32 info[16]
+constexpr uint32_t kRecWBytes = kJobRoundsW * kRoundWBytes;  // 3 KiB, also the descriptor staging
+constexpr uint32_t kClassLongW = 14;                       // class = 128-B step count below 14; 14: the rest
+constexpr uint32_t kClassNoneW = 15;                       // no packet
+constexpr int kFastWMax = (int)kClassLongW - 1;            // unrolled bodies up to 13 slots (1664 B)
+constexpr uint32_t kInstrStrideW = kWavesPerBlock * 1024;  // LDS bytes between a slot's two DMA areas
+constexpr uint32_t kMetaTopHi = 1u << 13;                  // the top word lies in chunk k + 4 (else chunk k)
+static_assert(kRecWBytes == kJobPacketsW * 12, "staging: u64 offsets + u32 lengths");
+static_assert(kJobRoundsW == 16, "round d of a workgroup: job d >> 4, round d & 15");
+
+struct JobSlotW {
+  u32x4 rec[kRecWBytes / 16];
+  uint32_t head[kJobRoundsW];  // per round: min steps | max steps << 8 | kHeadGeneric
+  uint32_t hist[16];           // job build: packets per class, then each class's first position
+  uint32_t res[kJobPacketsW];
+};
+struct RaggedWLds {
+  uint32_t tables[kRepDwords + 2 * 1024];  // replicated M32^16 | M32^1 block, then M32^4 and M32^8
+  u32x4 ring[kRingW][2][kWavesPerBlock][64];
+  JobSlotW job[kJobSlotsW];
+  uint32_t ready[kJobSlotsW];     // k + 1 once the workgroup's k-th job has its records here
+  uint32_t consumed[kJobSlotsW];  // rounds of the slot's job whose records have been read
+  uint32_t done[kJobSlotsW];      // rounds of the job whose checksums are in res
+  uint32_t freed[kJobSlotsW];     // k + 1 once the k-th job's checksums are in HBM
+  uint32_t next_dispatch;
+  uint32_t failed;                // != 0 once a wave gave up a wait (report_fault)
+};
+static_assert(sizeof(RaggedWLds) <= 160 * 1024, "LDS");
+
+// A lane's plan for one round: the sources of its two DMAs per slot (packets lane / 8 and
+// 8 + lane / 8, chunk lane % 8) and the state of its two Horner chunks (packet lane / 4,
+// chunks lane % 4 + 4 and lane % 4).
+struct RoundW {
+  uint64_t cb0, cb1;  // DMA: this lane's chunk address at slot 0, instruction 0 / 1 packet
+  int32_t top0, top1; // DMA: those packets' top slots (ns: no packet data)
+  uint32_t direct;    // DMA: bit i: instruction i's top chunk is read (inside, no fallback)
+  uint64_t cbc;       // compute: chunk k's address at slot 0 (chunk k + 4 lies 64 B below)
+  int32_t top_slot;   // compute: the packet's top slot
+  uint32_t meta;      // compute: head (of the chunk holding the top word), v, empty, z, store, fallback, kMetaTopHi
+  uint32_t last_mask; // compute: lane k == 0 clears the bytes past the packet end in the last word
+  uint32_t id;        // local id of the lane's packet in its job
+  int32_t ns;         // slots of the round (wave-uniform)
+  int32_t B;          // first top slot of a fast round
+  int32_t spread;     // max - min step count of the round's packets
+  bool fast, live;
+  uint32_t job_k, job_rounds;
+};
+
+// Source of instruction i's slot-s DMA (the zero chunk before the packet's top).
+__device__ __forceinline__ uint64_t srcw(const RoundW& r, int i, int32_t s, uint64_t dummy) {
+  const uint64_t cb = i ? r.cb1 : r.cb0;
+  const int32_t top = i ? r.top1 : r.top0;
+  const bool real = s > top || (s == top && ((r.direct >> i) & 1u));
+  return real ? cb + (uint64_t)kBytesPerStep * (uint64_t)s : dummy;
+}
+
+// DMA plan of one of the lane's two DMA packets (ragged_record fields, 128-B steps).
+__device__ __forceinline__ void dma_plan_w(uint64_t ax, uint32_t info, bool valid, int32_t ns, uint32_t k8,
+                                           const LaneConsts& c, uint64_t& cb, int32_t& top, bool& direct) {
+  const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
+  const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
+  const uint32_t pad = (info >> kRecPadShift) << 2;
+  cb = a1 - 16u * (uint64_t)(k8 + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(ns - 1);
+  top = ns - nsteps;
+  const int32_t rel = 112 - 16 * (int32_t)k8 - (int32_t)pad;  // chunk k8 at the top step, from the packet top
+  const bool inside = nsteps > 0 && rel > -16;
+  bool fb = false;
+  if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
+    const uint64_t t = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
+    fb = t - c.base4 < (uint64_t)(-rel);
+  }
+  direct = inside && !fb;
+}
+
+// A lane's round plan from the three records it reads and the round header.
+__device__ __forceinline__ RoundW roundw_from_records(uint64_t axc, uint32_t ic, uint64_t ax0, uint32_t i0,
+                                                      uint64_t ax1, uint32_t i1, bool rv, uint32_t hdr,
+                                                      const LaneConsts& c) {
+  const uint32_t lane = threadIdx.x & 63u, kc = lane & 3u, k8 = lane & 7u;
+  const bool vc = rv && ((axc >> kRecValidBit) & 1u);
+  const int32_t nsc = vc ? (int32_t)(ic & kRecStepsMask) : 0;
+  const int32_t nsmin = (int32_t)(hdr & 255u), nsmax = (int32_t)((hdr >> 8) & 255u);
+  const bool generic = (hdr & kHeadGeneric) != 0u || nsmax == 0;
+  int32_t mx = nsmax;
+  if (generic) {  // rare: the header does not bound the round
+    mx = __builtin_amdgcn_readlane(nsc, 0);
+#pragma unroll
+    for (int g = 1; g < kPW4; ++g) mx = max(mx, __builtin_amdgcn_readlane(nsc, g * kG4));
+  }
+  RoundW r;
+  r.ns = max(kRingW, mx);
+  bool d0, d1;
+  dma_plan_w(ax0, i0, rv && ((ax0 >> kRecValidBit) & 1u), r.ns, k8, c, r.cb0, r.top0, d0);
+  dma_plan_w(ax1, i1, rv && ((ax1 >> kRecValidBit) & 1u), r.ns, k8, c, r.cb1, r.top1, d1);
+  r.direct = (d0 ? 1u : 0u) | (d1 ? 2u : 0u);
+  // Compute side: chunks kc + 4 (rel1) and kc (rel1 + 64) at the top step, from the top.
+  const uint64_t a1 = vc ? (axc & kRecAddrMask) : c.base4;
+  const uint32_t pad = (ic >> kRecPadShift) << 2;
+  const uint32_t v = vc ? (uint32_t)(axc >> kRecVShift) & 3u : 0u;
+  const uint32_t z = vc ? (uint32_t)(axc >> kRecZShift) & 3u : 0u;
+  r.cbc = a1 - 16u * (uint64_t)(kc + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(r.ns - 1);
+  r.top_slot = r.ns - nsc;
+  const int32_t rel1 = 48 - 16 * (int32_t)kc - (int32_t)pad, rel0 = rel1 + 64;
+  const bool hi = nsc > 0 && rel1 > -16 && rel1 <= 0;  // the top word is in chunk kc + 4
+  const bool lo = nsc > 0 && rel0 > -16 && rel0 <= 0;  // ... in chunk kc
+  const int32_t rel = hi ? rel1 : rel0;
+  bool fb = false;
+  if (((axc >> kRecNearBit) & 1u) && vc && (hi || lo) && rel < 0) {
+    const uint64_t t = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsc - pad);
+    fb = t - c.base4 < (uint64_t)(-rel);
+  }
+  const uint32_t head = hi || lo ? (uint32_t)(rel / 4 + 4) : 0u;
+  r.meta = head | (v << kMetaVShift) | (nsc == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
+           (vc ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (hi ? kMetaTopHi : 0u);
+  r.last_mask = kc == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+  r.id = (uint32_t)(axc >> kJobLidShift4) & (uint32_t)(kJobPacketsW - 1);
+  r.B = r.ns - nsmax;
+  r.spread = nsmax - nsmin;
+  r.fast = !generic && r.ns <= kFastWMax && (r.ns == kRingW || r.spread <= 1);
+  return r;
+}
+
+// The ring of crc32_ragged16w_kernel: two positions of 2 KiB per wave (instruction 0's
+// 1 KiB, then instruction 1's kInstrStrideW further), in consumption order; the per-lane
+// offsets of the lane's two chunks inside a position; the landed data of the next slot.
+struct Ring2 {
+  uint32_t a0, a1;          // wave-uniform LDS byte addresses
+  uint32_t off_hi, off_lo;  // lane: chunk kc + 4 and chunk kc of its packet
+  u32x4 next_hi, next_lo;
+  template <int S>
+  __device__ __forceinline__ uint32_t at() const {
+    return S % 2 == 0 ? a0 : a1;
+  }
+  __device__ __forceinline__ uint32_t at_rt(uint32_t m) const { return m ? a1 : a0; }
+  __device__ __forceinline__ void rotate(uint32_t r) {
+    const uint32_t b0 = a0, b1 = a1;
+    a0 = r ? b1 : b0;
+    a1 = r ? b0 : b1;
+  }
+};
+
+// Wait until at most N DMAs are outstanding and read both chunks of the landed slot.
+template <int N>
+__device__ __forceinline__ void read_landed2(uint32_t addr_hi, uint32_t addr_lo, u32x4& hi, u32x4& lo) {
+  asm volatile(
+      "s_waitcnt vmcnt(%2)\n\t"
+      "ds_read_b128 %0, %3\n\t"
+      "ds_read_b128 %1, %4\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(hi), "=&v"(lo)
+      : "i"(N), "v"(addr_hi), "v"(addr_lo)
+      : "memory");
+}
+
+// h <- M(h) ^ w with the 16 lookups in one asm statement (no ring read).
+__device__ __forceinline__ void horner_step_lds(const Lookup& lk, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                                uint32_t& h3, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  uint32_t a[16];
+  const uint32_t hs[4] = {h0, h1, h2, h3};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[4 * j + t] = lookup_addr(hs[j], lk.lp, lk, t);
+  }
+  asm volatile(
+      "ds_read_b32 %4, %4\n\tds_read_b32 %5, %5\n\tds_read_b32 %6, %6\n\tds_read_b32 %7, %7\n\t"
+      "ds_read_b32 %8, %8\n\tds_read_b32 %9, %9\n\tds_read_b32 %10, %10\n\tds_read_b32 %11, %11\n\t"
+      "ds_read_b32 %12, %12\n\tds_read_b32 %13, %13\n\tds_read_b32 %14, %14\n\tds_read_b32 %15, %15\n\t"
+      "ds_read_b32 %16, %16\n\tds_read_b32 %17, %17\n\tds_read_b32 %18, %18\n\tds_read_b32 %19, %19\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_bitop3_b32 %4, %4, %5, %6 bitop3:0x96\n\t"
+      "v_bitop3_b32 %0, %4, %7, %20 bitop3:0x96\n\t"
+      "v_bitop3_b32 %8, %8, %9, %10 bitop3:0x96\n\t"
+      "v_bitop3_b32 %1, %8, %11, %21 bitop3:0x96\n\t"
+      "v_bitop3_b32 %12, %12, %13, %14 bitop3:0x96\n\t"
+      "v_bitop3_b32 %2, %12, %15, %22 bitop3:0x96\n\t"
+      "v_bitop3_b32 %16, %16, %17, %18 bitop3:0x96\n\t"
+      "v_bitop3_b32 %3, %16, %19, %23 bitop3:0x96"
+      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]),
+        "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]),
+        "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
+      : "v"(w0), "v"(w1), "v"(w2), "v"(w3)
+      : "memory");
+}
+
+// h <- M(h) ^ w fused with the next slot's two ring reads (vmcnt(N) before them).
+template <int N>
+__device__ __forceinline__ void horner_step_and_read2(const Lookup& lk, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                                      uint32_t& h3, uint32_t w0, uint32_t w1, uint32_t w2,
+                                                      uint32_t w3, uint32_t addr_hi, uint32_t addr_lo, u32x4& nhi,
+                                                      u32x4& nlo) {
+  uint32_t a[16];
+  const uint32_t hs[4] = {h0, h1, h2, h3};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[4 * j + t] = lookup_addr(hs[j], lk.lp, lk, t);
+  }
+  asm volatile(
+      "ds_read_b32 %6, %6\n\tds_read_b32 %7, %7\n\tds_read_b32 %8, %8\n\tds_read_b32 %9, %9\n\t"
+      "ds_read_b32 %10, %10\n\tds_read_b32 %11, %11\n\tds_read_b32 %12, %12\n\tds_read_b32 %13, %13\n\t"
+      "ds_read_b32 %14, %14\n\tds_read_b32 %15, %15\n\tds_read_b32 %16, %16\n\tds_read_b32 %17, %17\n\t"
+      "ds_read_b32 %18, %18\n\tds_read_b32 %19, %19\n\tds_read_b32 %20, %20\n\tds_read_b32 %21, %21\n\t"
+      "s_waitcnt vmcnt(%28)\n\t"
+      "ds_read_b128 %4, %22\n\t"
+      "ds_read_b128 %5, %23\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_bitop3_b32 %6, %6, %7, %8 bitop3:0x96\n\t"
+      "v_bitop3_b32 %0, %6, %9, %24 bitop3:0x96\n\t"
+      "v_bitop3_b32 %10, %10, %11, %12 bitop3:0x96\n\t"
+      "v_bitop3_b32 %1, %10, %13, %25 bitop3:0x96\n\t"
+      "v_bitop3_b32 %14, %14, %15, %16 bitop3:0x96\n\t"
+      "v_bitop3_b32 %2, %14, %17, %26 bitop3:0x96\n\t"
+      "v_bitop3_b32 %18, %18, %19, %20 bitop3:0x96\n\t"
+      "v_bitop3_b32 %3, %18, %21, %27 bitop3:0x96"
+      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(nhi), "=&v"(nlo), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]),
+        "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]),
+        "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
+      : "v"(addr_hi), "v"(addr_lo), "v"(w0), "v"(w1), "v"(w2), "v"(w3), "i"(N)
+      : "memory");
+}
+
+// The lane's top chunk (kc + 4 if kMetaTopHi, else kc) through its masks.
+__device__ __forceinline__ void mask_top_w(uint32_t meta, const TopMasks& m, uint32_t& x0, uint32_t& x1,
+                                           uint32_t& x2, uint32_t& x3, uint32_t& y0, uint32_t& y1, uint32_t& y2,
+                                           uint32_t& y3) {
+  if (meta & kMetaTopHi) {
+    x0 = and_xor(x0, m.am0, m.xm0);
+    x1 = and_xor(x1, m.am1, m.xm1);
+    x2 = and_xor(x2, m.am2, m.xm2);
+    x3 = and_xor(x3, m.am3, m.xm3);
+  } else {
+    y0 = and_xor(y0, m.am0, m.xm0);
+    y1 = and_xor(y1, m.am1, m.xm1);
+    y2 = and_xor(y2, m.am2, m.xm2);
+    y3 = and_xor(y3, m.am3, m.xm3);
+  }
+}
+
+// One slot of a fast round: refill this slot's ring position with slot S + 2 (two DMAs),
+// then the two Horner steps on the landed chunks (x = chunk kc + 4 first: it lies 64 B
+// below chunk kc in the packet), the second fused with the next slot's ring reads.  Lane
+// tops lie in slots B .. B + spread <= 1, issued by the previous round with per-lane
+// sources; slot B starts every stream (a stream is zero before its lane's top).
+template <int S, int NS, int B>
+__device__ __forceinline__ void roundw_slot(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
+                                            const TopMasks& m, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                            uint32_t& h3) {
+  constexpr int kF = S + kRingW;
+  const u32x4 vh = R.next_hi, vl = R.next_lo;
+  const uint32_t dst = R.at<S>();
+  if constexpr (kF < NS) {  // inside every packet of the round (kF > its top slot)
+    dma16(cur.cb0 + (uint64_t)kBytesPerStep * kF, dst);
+    dma16(cur.cb1 + (uint64_t)kBytesPerStep * kF, dst + kInstrStrideW);
+  } else {
+    dma16(srcw(nxt, 0, kF - NS, c.dummy), dst);
+    dma16(srcw(nxt, 1, kF - NS, c.dummy), dst + kInstrStrideW);
+  }
+  const uint32_t nb = R.at<S + 1>();
+  if constexpr (S < B) {
+    read_landed2<2 * (kRingW - 1)>(nb + R.off_hi, nb + R.off_lo, R.next_hi, R.next_lo);
+  } else {
+    uint32_t x0 = vh.x, x1 = vh.y, x2 = vh.z, x3 = vh.w;
+    uint32_t y0 = vl.x, y1 = vl.y, y2 = vl.z, y3 = vl.w;
+    if constexpr (S == NS - 1) y3 &= cur.last_mask;  // data only: before the injection
+    if constexpr (S < kRingW) {
+      if (NS == kRingW || S - B <= cur.spread) {
+        if (cur.top_slot == S) mask_top_w(cur.meta, m, x0, x1, x2, x3, y0, y1, y2, y3);
+      }
+    }
+    if constexpr (S == B) {
+      h0 = x0;  // M32^16(0) = 0: no lookups
+      h1 = x1;
+      h2 = x2;
+      h3 = x3;
+    } else {
+      horner_step_lds(c.lk, h0, h1, h2, h3, x0, x1, x2, x3);
+    }
+    horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h0, h1, h2, h3, y0, y1, y2, y3, nb + R.off_hi, nb + R.off_lo,
+                                            R.next_hi, R.next_lo);
+  }
+  issue_order_fence();
+}
+
+template <int NS, int B, int... S>
+__device__ __forceinline__ void roundw_slots(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
+                                             const TopMasks& m, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                             uint32_t& h3, std::integer_sequence<int, S...>) {
+  (roundw_slot<S, NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3), ...);
+}
+
+template <int NS, int B>
+__device__ __forceinline__ void roundw_fast(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
+                                            uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  static_assert(B == 0 || NS == kRingW, "leading consumed slots only in ring-length rounds");
+  const TopMasks m = top_masks(cur.meta);
+  roundw_slots<NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3, std::make_integer_sequence<int, NS>{});
+  R.rotate((uint32_t)(NS % 2));
+}
+
+// Any round (wider spreads, longer packets, chunks below the caller's buffer, a job's
+// partial last round): per-lane top slots and sources, runtime slot count.
+__device__ __forceinline__ void roundw_generic(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
+                                               uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  const TopMasks tm = top_masks(cur.meta);
+  uint32_t m = 0;  // s % 2
+  for (int32_t s = 0; s < cur.ns; ++s) {
+    const u32x4 vh = R.next_hi, vl = R.next_lo;
+    const int32_t f = s + kRingW;
+    const uint32_t dst = R.at_rt(m);
+    if (f < cur.ns) {
+      dma16(srcw(cur, 0, f, c.dummy), dst);
+      dma16(srcw(cur, 1, f, c.dummy), dst + kInstrStrideW);
+    } else {
+      dma16(srcw(nxt, 0, f - cur.ns, c.dummy), dst);
+      dma16(srcw(nxt, 1, f - cur.ns, c.dummy), dst + kInstrStrideW);
+    }
+    m ^= 1u;
+    uint32_t x0 = vh.x, x1 = vh.y, x2 = vh.z, x3 = vh.w;
+    uint32_t y0 = vl.x, y1 = vl.y, y2 = vl.z, y3 = vl.w;
+    const bool top = s == cur.top_slot;
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
+      if (top && (cur.meta & kMetaFallback)) {
+        const uint64_t ca = cur.cbc + (uint64_t)kBytesPerStep * (uint64_t)s;
+        if (cur.meta & kMetaTopHi)
+          load_top_words(ca - 64u, cur.meta, c.dummy, x0, x1, x2, x3);
+        else
+          load_top_words(ca, cur.meta, c.dummy, y0, y1, y2, y3);
+      }
+    }
+    if (s == cur.ns - 1) y3 &= cur.last_mask;  // data only: before the injection
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+      if (top) mask_top_w(cur.meta, tm, x0, x1, x2, x3, y0, y1, y2, y3);
+    }
+    horner_step_lds(c.lk, h0, h1, h2, h3, x0, x1, x2, x3);
+    const uint32_t nb = R.at_rt(m);
+    horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h0, h1, h2, h3, y0, y1, y2, y3, nb + R.off_hi, nb + R.off_lo,
+                                            R.next_hi, R.next_lo);
+    issue_order_fence();
+  }
+  R.rotate(m);
+}
+
+template <int... I>
+__device__ __forceinline__ bool roundw_dispatch(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
+                                                uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3,
+                                                std::integer_sequence<int, I...>) {
+  if (cur.ns == kRingW) {
+    if (cur.B == 0) roundw_fast<kRingW, 0>(cur, nxt, R, c, h0, h1, h2, h3);
+    else if (cur.B == 1) roundw_fast<kRingW, 1>(cur, nxt, R, c, h0, h1, h2, h3);
+    else return false;
+    return true;
+  }
+  return ((cur.ns == I + kRingW + 1 ? (roundw_fast<I + kRingW + 1, 0>(cur, nxt, R, c, h0, h1, h2, h3), true)
+                                    : false) ||
+          ...);
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16w_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
+  send_servers_home();
+  __shared__ __attribute__((aligned(16))) RaggedWLds S;
+  uint32_t* const lds = S.tables;
+  constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
+  if (threadIdx.x < (unsigned)kJobSlotsW) {
+    S.ready[threadIdx.x] = 0;
+    S.consumed[threadIdx.x] = 0;
+    S.done[threadIdx.x] = 0;
+    S.freed[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) {
+    S.next_dispatch = kWavesPerBlock * kLook;
+    S.failed = 0;
+  }
+  fill_lds4(lds);
+  __syncthreads();
+  const LaneConsts c = lane_consts(b.base);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t kc = lane & 3u, pc = lane >> 2, p8 = lane >> 3;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // fused lookups use raw addresses
+
+  auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
+  auto job_count = [&](uint64_t J) -> uint32_t {  // packets in job J (J < njobs)
+    const uint64_t left = b.count - J * kJobPacketsW;
+    return left < (uint64_t)kJobPacketsW ? (uint32_t)left : (uint32_t)kJobPacketsW;
+  };
+  auto round_valid = [&](uint32_t d) -> bool {
+    const uint64_t J = job_of(d >> 4);
+    return J < b.njobs && (d & 15u) * kPW4 < job_count(J);
+  };
+
+  // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0, u32
+  // lengths at +2048): three 16-B DMAs per lane, or, near the batch end, 12 4-B DMAs
+  // clamped to the batch.
+  auto job_dma = [&](uint64_t J, uint32_t slot) {
+    LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
+    const uint64_t p0 = J * kJobPacketsW;
+    if (p0 + kJobPacketsW <= b.count) {
+      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 2 * lane), (LdsVoid*)st, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 + 2 * lane), (LdsVoid*)(st + 1024), 16, 0,
+                                       0);
+      __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 4 * lane), (LdsVoid*)(st + 2048), 16, 0, 0);
+    } else {
+      const uint32_t* offw = reinterpret_cast<const uint32_t*>(b.offsets);
+#pragma unroll 1
+      for (uint32_t i = 0; i < 12; ++i) {
+        const uint32_t w = 64u * (i & 7u) + lane;
+        const uint64_t e = i < 8 ? p0 + w / 2 : p0 + 64u * (i - 8u) + lane;
+        const void* src = e >= b.count ? (const void*)g_zero_chunk
+                          : i < 8    ? (const void*)(offw + 2 * e + (w & 1u))
+                                     : (const void*)(b.lengths + e);
+        __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 256 * i), 4, 0, 0);
+      }
+    }
+  };
+  // Phase B (after a round body: every DMA but the last two has landed): sort the job's
+  // packets by 128-B step class (LDS histogram, as in crc32_ragged16_kernel), write its
+  // round records and headers in place of the descriptors, then mark the slot ready.
+  auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
+    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(2 * (kRingW - 1)) : "memory");
+    const uint32_t st = lds_addr(&S.job[slot].rec[0]);
+    const uint32_t hd = lds_addr(&S.job[slot].head[0]);
+    const uint32_t hi = lds_addr(&S.job[slot].hist[0]);
+    const uint32_t n = job_count(J);
+    uint32_t ln4;  // lane * 4 from asm: not hoisted out of the round loop
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 2, %0"
+                 : "=v"(ln4));
+    if (lane < 16u) {
+      lds_st32_nowait(hi + 4u * lane, 0u);
+      lds_st32_nowait(hd + 4u * lane, 0u);
+    }
+    const u32x4 o01 = lds_ld128(st + 8u * ln4), o23 = lds_ld128(st + 8u * ln4 + 16u);
+    const u32x4 ll = lds_ld128(st + 2048u + 4u * ln4);
+    const uint64_t off[4] = {o01.x | (uint64_t)o01.y << 32, o01.z | (uint64_t)o01.w << 32,
+                             o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
+    const uint32_t len[4] = {ll.x, ll.y, ll.z, ll.w};
+    uint64_t ax[4];
+    uint32_t info[4], cls[4], pos[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t id = ln4 + (uint32_t)i;
+      const bool v = id < n;
+      const RaggedRecord rec = ragged_record(b.base + off[i], len[i], c.base4);
+      ax[i] = v ? rec.ax | ((uint64_t)id << kJobLidShift4) : 0ull;
+      info[i] = rec.info;
+      const bool lng = rec.nsteps >= kClassLongW || ((rec.ax >> kRecNearBit) & 1u);
+      cls[i] = !v ? kClassNoneW : (lng ? kClassLongW : rec.nsteps);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pos[i] = lds_add_rtn(hi + 4u * cls[i], 1u);
+    uint32_t cnt = 0;
+    if (lane < 16u) cnt = lds_ld32(hi + 4u * lane);
+    const uint32_t first = wave_inclusive_add(cnt) - cnt;
+    if (lane < 16u) lds_st32(hi + 4u * lane, first);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t q = lds_ld32(hi + 4u * cls[i]) + pos[i];
+      const uint32_t r = st + (q >> 4) * kRoundWBytes;
+      lds_st64(r + 8u * (q & 15u), ax[i]);
+      lds_st32(r + 128u + 4u * (q & 15u), info[i]);
+      if (cls[i] != kClassNoneW) {
+        const uint32_t h = hd + 4u * (q >> 4);
+        const uint32_t ns8 = min(info[i] & kRecStepsMask, 255u);
+        if ((q & 15u) == 0u) lds_st8_nowait(h, ns8);
+        if ((q & 15u) == 15u || q + 1u == n) lds_st8_nowait(h + 1u, ns8);
+        // Longer packets, chunks near the caller's base, and the job's partial last round
+        // (its empty groups' chunk addresses lie below the base) take the generic body.
+        if (cls[i] == kClassLongW || ((q & 15u) != 15u && q + 1u == n)) lds_or_nowait(h, kHeadGeneric);
+      }
+    }
+    if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);  // waits for every LDS write above
+  };
+
+  // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
+  // (rounds 0 .. 31: jobs 0 and 1) and kJobAheadW more.
+  const uint32_t first_jobs = (kWavesPerBlock * kLook - 1) / kJobRoundsW + kJobAheadW + 1;
+  static_assert((kWavesPerBlock * kLook - 1) / kJobRoundsW + kJobAheadW + 1 <= kJobSlotsW, "prologue jobs");
+  if (wv < first_jobs && job_of(wv) < b.njobs) {
+    job_dma(job_of(wv), wv);
+    __builtin_amdgcn_s_waitcnt(0);
+    job_build(job_of(wv), wv, wv + 1u);
+  }
+  __syncthreads();
+
+  uint32_t seen_ready = 0, seen_freed = 0;
+  const uint32_t fail_a = lds_addr(&S.failed);
+  auto waited = [&](uint32_t w, uint32_t bit) -> bool {
+    if (w == kWaitGaveUp) report_fault(fail_a, bit);
+    return w == kWaitOk;
+  };
+  auto make_round = [&](uint32_t d) -> RoundW {
+    uint64_t axc = 0, ax0 = 0, ax1 = 0;
+    uint32_t ic = 0, i0 = 0, i1 = 0, hdr = 0;
+    const uint32_t k = d >> 4, slot = k & (uint32_t)(kJobSlotsW - 1), rj = d & 15u;
+    const uint64_t J = job_of(k);
+    const uint32_t n = J < b.njobs ? job_count(J) : 0u;
+    const bool live = rj * kPW4 < n;  // round_valid(d)
+    bool rv = live;
+    if (rv && k + 1u > seen_ready) {
+      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
+      if (rv) seen_ready = k + 1u;
+    }
+#ifdef ENET_CRC_TEST_HOOKS
+    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k) rv = waited(kWaitGaveUp, kFaultReady);
+#endif
+    if (rv) {
+      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + rj * kRoundWBytes;
+      asm volatile(
+          "ds_read_b64 %0, %7\n\tds_read_b32 %1, %8\n\t"
+          "ds_read_b64 %2, %9\n\tds_read_b32 %3, %10\n\t"
+          "ds_read_b64 %4, %11\n\tds_read_b32 %5, %12\n\t"
+          "ds_read_b32 %6, %13\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(axc), "=&v"(ic), "=&v"(ax0), "=&v"(i0), "=&v"(ax1), "=&v"(i1), "=&v"(hdr)
+          : "v"(r + 8u * pc), "v"(r + 128u + 4u * pc), "v"(r + 8u * p8), "v"(r + 128u + 4u * p8),
+            "v"(r + 64u + 8u * p8), "v"(r + 160u + 4u * p8), "v"(lds_addr(&S.job[slot].head[rj]))
+          : "memory");
+      hdr = __builtin_amdgcn_readfirstlane(hdr);
+      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
+    }
+    RoundW rr = roundw_from_records(axc, ic, ax0, i0, ax1, i1, rv, hdr, c);
+    rr.live = live;
+    rr.job_k = k;
+    rr.job_rounds = (n + kPW4 - 1) / kPW4;
+    return rr;
+  };
+
+  uint32_t rnd1 = wv + kWavesPerBlock;
+  if (!round_valid(wv)) return;
+  RoundW cur = make_round(wv);
+  RoundW nxt = make_round(rnd1);
+  Ring2 R;
+  R.a0 = lds_addr(&S.ring[0][0][wv][0]);
+  R.a1 = lds_addr(&S.ring[1][0][wv][0]);
+  R.off_lo = (pc >> 3) * kInstrStrideW + 16u * (8u * (pc & 7u) + kc);
+  R.off_hi = R.off_lo + 64u;
+  dma16(srcw(cur, 0, 0, c.dummy), R.a0);  // cur.ns >= kRingW
+  dma16(srcw(cur, 1, 0, c.dummy), R.a0 + kInstrStrideW);
+  dma16(srcw(cur, 0, 1, c.dummy), R.a1);
+  dma16(srcw(cur, 1, 1, c.dummy), R.a1 + kInstrStrideW);
+  read_landed2<2 * (kRingW - 1)>(R.a0 + R.off_hi, R.a0 + R.off_lo, R.next_hi, R.next_lo);
+  while (cur.live) {
+    uint32_t d = 0;
+    if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
+    d = __builtin_amdgcn_readfirstlane(d);
+    // Build duty: the claimer of a job's first round builds the job kJobAheadW later once
+    // every round of the slot's previous job has read its record (crc32_ragged_jobs_kernel).
+    bool build = false;
+    const uint32_t kb = (d >> 4) + kJobAheadW, bslot = kb & (uint32_t)(kJobSlotsW - 1);
+    if ((d & 15u) == 0u && kb >= first_jobs && job_of(kb) < b.njobs) {
+      build = kb < (uint32_t)kJobSlotsW ||
+              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), kJobRoundsW, fail_a), kFaultConsumed);
+      if (build) {
+        if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
+        job_dma(job_of(kb), bslot);
+      }
+    }
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    if (!cur.fast || !roundw_dispatch(cur, nxt, R, c, h0, h1, h2, h3,
+                                      std::make_integer_sequence<int, kFastWMax - kRingW>{}))
+      roundw_generic(cur, nxt, R, c, h0, h1, h2, h3);
+    const uint32_t y = combine_tree4(lds, h0, h1, h2, h3, c.lk);
+    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane kc == 0 holds it
+    if (cur.meta & kMetaEmpty) reg = kInitRegister;
+    const uint32_t k0 = cur.job_k, slot0 = k0 & (uint32_t)(kJobSlotsW - 1);
+    if (k0 >= (uint32_t)kJobSlotsW && k0 + 1u - (uint32_t)kJobSlotsW > seen_freed) {
+      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlotsW + 1u, fail_a), kFaultFreed))
+        seen_freed = k0 + 1u - (uint32_t)kJobSlotsW;
+    }
+    if (kc == 0 && (cur.meta & kMetaStore))
+      lds_st32_nowait(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
+    uint32_t old = 0;
+    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old + 1u == cur.job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
+      const uint64_t J0 = job_of(k0);
+      const uint32_t n0 = job_count(J0);
+      const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
+      uint32_t* dst = out + J0 * kJobPacketsW + 4u * lane;
+      if (4u * lane + 4u <= n0) {
+        reinterpret_cast<U32x4A4*>(dst)->v = v;
+      } else {
+        if (4u * lane + 0u < n0) dst[0] = v.x;
+        if (4u * lane + 1u < n0) dst[1] = v.y;
+        if (4u * lane + 2u < n0) dst[2] = v.z;
+      }
+    }
+    if (old + 1u == cur.job_rounds && lane == 0) {
+      lds_st32(lds_addr(&S.done[slot0]), 0u);
+      lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
+    }
+    if (build) job_build(job_of(kb), bslot, kb + 1u);
+    const RoundW after = make_round(d);
     cur = nxt;
     nxt = after;
   }
@@ -2815,15 +3430,17 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
   // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
   // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
-#ifndef ENET_CRC_RAGGED16
-  constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds;
+#if defined(ENET_CRC_RAGGED16W)  // fixed jobs of 16 rounds (the kernel's d >> 4)
+  constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRoundsW, kMinJobRounds = kJobRoundsW;
+#elif defined(ENET_CRC_RAGGED16)
+  constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRounds4, kMinJobRounds = kJobRounds4 / 2;
 #else
-  constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRounds4;
+  constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds, kMinJobRounds = kJobRounds / 2;
 #endif
   const int cus = cu_count_for_current_device();
   if (cus <= 0) return hipErrorNoDevice;
   uint64_t jp = kMaxJobRounds * kRoundPackets, njobs = 0, best = ~0ull;
-  for (uint64_t rj = kMaxJobRounds; rj >= kMaxJobRounds / 2; --rj) {
+  for (uint64_t rj = kMaxJobRounds; rj >= kMinJobRounds; --rj) {
     const uint64_t p = rj * kRoundPackets, nj = (count + p - 1) / p;
     const uint64_t grid = nj < (uint64_t)cus ? nj : (uint64_t)cus;
     const uint64_t span = (nj + grid - 1) / grid * rj;
@@ -2853,10 +3470,12 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
   jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
 #endif
-#ifndef ENET_CRC_RAGGED16
-  hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
-#else
+#if defined(ENET_CRC_RAGGED16W)
+  hipLaunchKernelGGL(crc32_ragged16w_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+#elif defined(ENET_CRC_RAGGED16)
   hipLaunchKernelGGL(crc32_ragged16_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+#else
+  hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
 #endif
   return hipGetLastError();
 }

@@ -14,7 +14,7 @@
 // warm-up; prints us per launch and GB/s.  Addresses stay inside the buffer: the packets
 // start 4 KiB into the allocation and a chunk never reaches more than 128 B before a packet.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/dma_shape tools/dma_shape.hip
-//   tools/dma_shape [L=1392] [packets=1605632] [base_offset=0]
+//   tools/dma_shape [L=1392] [packets=1605632] [base_offset=0] [align: 16 rounds every lane load down to 16 B]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -48,7 +48,7 @@ __device__ __forceinline__ u32x4 read_lds(uint32_t addr) {
 // P packets per round, PIECE bytes per packet per slot, I instructions per slot, ring of D.
 template <int P, int PIECE, int I, int D>
 __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32_t L, uint64_t rounds,
-                                                     uint32_t* out) {
+                                                     uint64_t amask, uint32_t* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   constexpr int kLanesPerPkt = PIECE / 16;
   static_assert(P * PIECE == 1024 * I, "a slot is I KiB");
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32
     const uint32_t t = ns - 1 - s;
     const uint32_t pkt = i * (64 / kLanesPerPkt) + lane / kLanesPerPkt, k = lane % kLanesPerPkt;
     const uint8_t* end = base + (r * P + pkt + 1) * (uint64_t)L;
-    return end - (uint64_t)PIECE * (t + 1) + 16 * k;
+    return (const uint8_t*)((uint64_t)(end - (uint64_t)PIECE * (t + 1) + 16 * k) & amask);
   };
   uint64_t dj = 0;
   uint32_t dsl = 0;
@@ -107,12 +107,12 @@ __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32
 struct Shape {
   const char* name;
   int P;
-  void (*launch)(int grid, const uint8_t*, uint32_t, uint64_t, uint32_t*);
+  void (*launch)(int grid, const uint8_t*, uint32_t, uint64_t, uint64_t, uint32_t*);
 };
 
 template <int P, int PIECE, int I, int D>
-void launch_shape(int grid, const uint8_t* b, uint32_t L, uint64_t rounds, uint32_t* out) {
-  hipLaunchKernelGGL((shape_kernel<P, PIECE, I, D>), dim3(grid), dim3(1024), 0, 0, b, L, rounds, out);
+void launch_shape(int grid, const uint8_t* b, uint32_t L, uint64_t rounds, uint64_t amask, uint32_t* out) {
+  hipLaunchKernelGGL((shape_kernel<P, PIECE, I, D>), dim3(grid), dim3(1024), 0, 0, b, L, rounds, amask, out);
 }
 
 #define CHECK(x)                                                             \
@@ -128,6 +128,8 @@ int main(int argc, char** argv) {
   const uint32_t L = argc > 1 ? (uint32_t)atoi(argv[1]) : 1392;
   uint64_t n = argc > 2 ? strtoull(argv[2], nullptr, 10) : 1605632;
   const uint32_t off = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
+  // align=16: every 16-B lane load rounded down to a 16-B boundary (same pattern otherwise)
+  const uint64_t amask = argc > 4 && atoi(argv[4]) == 16 ? ~(uint64_t)15 : ~(uint64_t)0;
   n -= n % 16;
   if (L < 16 || L > 65536 || off > 64) return 1;
   const Shape shapes[] = {
@@ -149,10 +151,10 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  printf("L=%u packets=%llu bytes=%llu base_offset=%u grid=%d\n", L, (unsigned long long)n,
-         (unsigned long long)bytes, off, grid);
+  printf("L=%u packets=%llu bytes=%llu base_offset=%u align=%s grid=%d\n", L, (unsigned long long)n,
+         (unsigned long long)bytes, off, amask == ~(uint64_t)0 ? "none" : "16", grid);
   // warm-up through the power-management transient
-  for (int w = 0; w < 60; ++w) shapes[w % ns].launch(grid, base, L, n / shapes[w % ns].P, out);
+  for (int w = 0; w < 60; ++w) shapes[w % ns].launch(grid, base, L, n / shapes[w % ns].P, amask, out);
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   std::vector<std::vector<float>> us(ns);
@@ -160,9 +162,9 @@ int main(int argc, char** argv) {
   for (int blk = 0; blk < kBlocks; ++blk)
     for (int j = 0; j < ns; ++j) {
       const int s = blk % 2 ? ns - 1 - j : j;
-      shapes[s].launch(grid, base, L, n / shapes[s].P, out);
+      shapes[s].launch(grid, base, L, n / shapes[s].P, amask, out);
       CHECK(hipEventRecord(e0, 0));
-      for (int it = 0; it < kLaunches; ++it) shapes[s].launch(grid, base, L, n / shapes[s].P, out);
+      for (int it = 0; it < kLaunches; ++it) shapes[s].launch(grid, base, L, n / shapes[s].P, amask, out);
       CHECK(hipEventRecord(e1, 0));
       CHECK(hipEventSynchronize(e1));
       float ms = 0;
