@@ -625,6 +625,27 @@ __device__ __forceinline__ RaggedRecord ragged_record(uint64_t sa, uint32_t len,
   return r;
 }
 
+// ragged_record with 16-B-aligned chunks (crc32_ragged_jobs_kernel under ENET_CRC_RAGGED_A16):
+// the packet runs on from a1 to the next 16-B boundary A1, u = (A1 - a1) / 4 more zero words
+// (u << kRecUShift in ax), so that every chunk address A1 - 16 (k + 1) - 128 i is 16-B
+// aligned.  A chunk then never leaves the 16-B blocks holding packet bytes (no fallback: near
+// is 0), and the round end takes the register back over the u words with M32^-1.
+constexpr int kRecUShift = 62;
+__device__ __forceinline__ RaggedRecord ragged_record_a16(uint64_t sa, uint32_t len) {
+  const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
+  const uint64_t a1x = sa + len + z, a1 = len ? (a1x + 15u) & ~(uint64_t)15 : a1x;
+  const uint64_t top = sa & ~(uint64_t)3;
+  const uint32_t nwords = (uint32_t)((a1 - top) >> 2);
+  const uint32_t nsteps = (nwords + 31u) >> 5;
+  const uint32_t pad = 128u * nsteps - 4u * nwords;  // 0..124
+  RaggedRecord r;
+  r.ax = a1 | ((sa & 3u) << kRecVShift) | ((uint64_t)z << kRecZShift) | (1ull << kRecValidBit) |
+         ((a1 - a1x) >> 2) << kRecUShift;
+  r.info = nsteps | ((pad >> 2) << kRecPadShift);
+  r.nsteps = nsteps;
+  return r;
+}
+
 // Inclusive prefix sum over the 64 lanes in DPP (no LDS round trips): shifts of 1, 2, 4
 // and 8 inside each 16-lane row, then row 0's and row 1's last lanes broadcast into the
 // rows above (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).
@@ -1493,6 +1514,11 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
             (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
   rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+#ifdef ENET_CRC_RAGGED_A16
+  // The zero words past the packet (16-B-aligned chunks): lane k == 0 masks them off in the
+  // last slot (mask_last) and takes the register back over them (back_over_padding).
+  if (valid && c.k == 0) rr.meta |= (uint32_t)(ax >> kRecUShift) << kMetaTShiftShift;
+#endif
   rr.id = id;
   // Fast: every packet starts at the same slot (same step count), no fallback chunk,
   // and the lanes whose top chunk lies before their packet are exactly the ones the
@@ -1525,6 +1551,24 @@ struct RaggedRing {
   __device__ __forceinline__ uint32_t next_addr() const { return ring0 + q * kRingStride + lane16; }
 };
 
+// The packet's last word (lane k == 0, last slot): the bytes past the packet end cleared;
+// with 16-B-aligned chunks (ENET_CRC_RAGGED_A16) the u words after it are zero as well.
+__device__ __forceinline__ void mask_last(const RaggedRound& r, uint32_t& w0, uint32_t& w1, uint32_t& w2,
+                                          uint32_t& w3) {
+#ifdef ENET_CRC_RAGGED_A16
+  const uint32_t u = (r.meta >> kMetaTShiftShift) & 3u, lm = r.last_mask;
+  w3 = u == 0 ? w3 & lm : 0u;
+  w2 = u == 1 ? w2 & lm : (u > 1 ? 0u : w2);
+  w1 = u == 2 ? w1 & lm : (u > 2 ? 0u : w1);
+  w0 = u == 3 ? w0 & lm : w0;
+#else
+  (void)w0;
+  (void)w1;
+  (void)w2;
+  w3 &= r.last_mask;
+#endif
+}
+
 // A round in which every packet has the same step count and needs no fallback: the
 // slot loop of crc32_uniform_dma_kernel (unrolled, lookups fused with the next ring
 // read); slot T (the packets' top slot) masks the top words, the last slot the bytes
@@ -1546,7 +1590,7 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
       continue;
     }
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    if (s == NS - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
+    if (s == NS - 1) mask_last(cur, w0, w1, w2, w3);  // data only: before the injection in mask_top
     if (s == T) {
       if (__builtin_amdgcn_ballot_w64(cur.meta & kMetaHeadMask)) {
         if (cur.meta & kMetaHeadMask) mask_top(cur.meta, w0, w1, w2, w3);
@@ -1597,7 +1641,7 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
       if (top && (cur.meta & kMetaFallback))
         load_top_words(cur.cb + (uint64_t)kStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
     }
-    if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
+    if (s == cur.ns - 1) mask_last(cur, w0, w1, w2, w3);  // data only: before the injection in mask_top
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
       if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
     }
@@ -1657,6 +1701,9 @@ struct JobSlot {
 };
 struct RaggedJobsLds {
   uint32_t tables[kLdsDwords];
+#ifdef ENET_CRC_RAGGED_A16
+  uint32_t inv[1024];  // M32^-1 (back_over_padding)
+#endif
   u32x4 ring[kRaggedRing][kWavesPerBlock][64];
   JobSlot job[kJobSlots];
   uint32_t ready[kJobSlots];     // k + 1 once the workgroup's k-th job has its records here
@@ -1760,6 +1807,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     S.failed = 0;
   }
   fill_lds(lds);
+#ifdef ENET_CRC_RAGGED_A16
+  for (int x = threadIdx.x; x < 1024; x += kBlock) S.inv[x] = g_op_tables.inv1[x >> 8][x & 255];
+#endif
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1830,7 +1880,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool v = 4u * lane + i < n;
+#ifdef ENET_CRC_RAGGED_A16
+      const RaggedRecord rec = ragged_record_a16(b.base + off[i], len[i]);
+#else
       const RaggedRecord rec = ragged_record(b.base + off[i], len[i], c.base4);
+#endif
       ax[i] = v ? rec.ax | ((uint64_t)(4u * lane + i) << kJobLidShift) : 0ull;
       info[i] = rec.info;
       cls[i] = v ? (rec.nsteps < kStepClasses - 1 ? rec.nsteps : kStepClasses - 1) : (uint32_t)kStepClasses;
@@ -1971,7 +2025,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     st_body += st_b1 - st_b0;
     ++st_rounds;
 #endif
-    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+    uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
+#ifdef ENET_CRC_RAGGED_A16
+    {  // back over the u zero words past the packet: y <- M32^-u y (lane k == 0, u = 0..3)
+      const uint32_t u = (cur.meta >> kMetaTShiftShift) & 3u;
+      if (u) {
+        y = apply_small(S.inv, y);
+        if (u > 1u) y = apply_small(S.inv, y);
+        if (u > 2u) y = apply_small(S.inv, y);
+      }
+    }
+#endif
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
 #ifdef ENET_CRC_ROUND_STAMPS

@@ -35,6 +35,7 @@ struct OpTables {
   uint32_t op[kOpLevels][4][256];
   uint32_t head_k[4];
   uint8_t inv_top[256];  // inv_top[sarwate[b] >> 24] = b (see m8_inverse)
+  uint32_t inv1[4][256];  // M32^-1 (back over one zero word), same four-table form
 };
 
 constexpr uint32_t sarwate_entry(uint32_t b) {
@@ -79,6 +80,17 @@ constexpr OpTables make_op_tables() {
     }
   }
   for (uint32_t b = 0; b < 256; ++b) t.inv_top[t.sarwate[b] >> 24] = (uint8_t)b;
+  // M32^-1 = M8^-4, one byte step back at a time through inv_top (m8_inverse in O(1)).
+  for (int k = 0; k < 4; ++k) {
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t y = b << (8 * k);
+      for (int s = 0; s < 4; ++s) {
+        const uint32_t i = t.inv_top[y >> 24];
+        y = ((y ^ t.sarwate[i]) << 8) | i;
+      }
+      t.inv1[k][b] = y;
+    }
+  }
   uint32_t k = kInitRegister;
   t.head_k[0] = k;
   for (int v = 1; v < 4; ++v) {

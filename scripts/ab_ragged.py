@@ -5,7 +5,8 @@
 
 Both builds are loaded side by side (ctypes, RTLD_LOCAL: each keeps its own kernels) and
 called through enet_crc32_ragged_device on the same device buffers: G2 (1M x U[64,1392],
-BASELINE configs[2]) and frag_64k (32,768 x 64 KiB payloads as 49 datagrams each).  Both
+BASELINE configs[2]) and frag_64k (32,768 x 64 KiB payloads as 49 datagrams each); rNNN = 1M datagrams of NNN
+bytes through the ragged entry; g1 / mtu through the uniform entry.  Both
 outputs are checked against each other in full and against the oracle on a sample; then
 blocks of `launches` back-to-back launches alternate A, B, A, B, ... after a read-ceiling
 warm-up, timed with HIP events on the launch stream.  Prints per-block kernel us and the
@@ -62,6 +63,8 @@ def main() -> int:
         uniform = name in ("g1", "mtu")
         if name == "g2":
             lengths = ragged_lengths(ENET_SEED, 1 << 20)
+        elif name.startswith("r") and name[1:].isdigit():  # ragged API, one length (e.g. r740)
+            lengths = np.full(1 << 20, int(name[1:]), dtype=np.uint32)
         elif uniform:
             lengths = np.full(1 << 20, 1200 if name == "g1" else 1392, dtype=np.uint32)
         else:

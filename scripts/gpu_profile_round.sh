@@ -62,6 +62,8 @@ for spec in "20 5" "200 10"; do
   set -- $spec
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_$1_$2" -o run \
     -- python3 "$ROOT/bench.py" --steps $1 --warmup $2 --cpu-seconds 0 --no-e2e --no-shard > "$OUT/trace_$1_$2.json" 2> "$OUT/trace_$1_$2.err") || exit $?
+  python3 scripts/trace_vs_line.py "$OUT/trace_$1_$2" "$OUT/trace_$1_$2.json" --csv "$OUT/trace_$1_$2_kernel_trace.csv" \
+    > "$OUT/trace_$1_$2_vs_line.json" 2>&1
 done
 echo "[profile] launch traces done" >&2
 echo "[profile] done" >&2

@@ -12,3 +12,4 @@ ENET_CRC_AMD_LIB=$GRAFT_REPO_ROOT/$V timeout -k 10 600 python -u -m pytest tests
 tail -2 $O/pytest_gpu_ring2.log
 timeout -k 10 200 python -u scripts/ab_ragged.py $V $P --configs g2,frag > $O/ab_ring2.txt 2>&1 || { cat $O/ab_ring2.txt; exit 1; }
 grep -v amdgpu.ids $O/ab_ring2.txt | grep -v '^{'
+bash scripts/gpu_r04_a16.sh ${1:-r04_ring2} || exit $?

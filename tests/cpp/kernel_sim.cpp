@@ -6,7 +6,9 @@
 // count the kernel template allows, without a GPU.  kExt models the LDS-DMA kernels'
 // trailing-byte handling: the packet runs to the next 4-byte boundary with the bytes
 // past its end masked to zero, and the last word's shift stops z bytes short
-// (finish_word: M8^(4-z) y from the M32^1 tables, instead of M32 y).
+// (finish_word: M8^(4-z) y from the M32^1 tables, instead of M32 y).  kA16 (with kExt)
+// models 16-B-aligned chunks: the packet runs on to the next 16-B boundary, u = 0..3 more
+// zero words, and the combined value goes back over them with M32^-1 before finish_word.
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -27,14 +29,18 @@ static const OpTables& T = kOpTables;
 
 static uint32_t op(int lv, uint32_t x) { return apply_op(T.op[lv], x); }
 
-template <int G, bool kExt = false>
+template <int G, bool kExt = false, bool kA16 = false>
 static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
+  static_assert(!kA16 || kExt, "16-B chunks only in the extended form");
   const uint64_t z = kExt && len ? (4 - ((s + len) & 3)) & 3 : 0;
-  const uint64_t sa = s, ea = s + len, top = sa & ~3ull, a1 = kExt ? (ea + z) : (ea & ~3ull);
+  const uint64_t sa = s, ea = s + len, top = sa & ~3ull, a1x = kExt ? (ea + z) : (ea & ~3ull);
+  const uint64_t a1 = kA16 && len ? (a1x + 15) & ~15ull : a1x;
+  const uint32_t u = (uint32_t)((a1 - a1x) >> 2);  // zero words past the packet's last word
   // Word at byte address a (a >= top): the packet's bytes, zeros past its end (kExt).
   auto word_at = [&](uint64_t a) {
     uint32_t w = 0;
     memcpy(&w, buf + a, 4);
+    if (kExt && a >= ea) return 0u;
     if (kExt && a + 4 > ea) w &= 0xFFFFFFFFu >> (8 * (a + 4 - ea));
     return w;
   };
@@ -75,7 +81,9 @@ static uint32_t model(const uint8_t* buf, uint64_t s, uint64_t len) {
       // finish_word: M8^(4-z)(y) = M32(y << 8z) ^ (y >> (32 - 8z)): the bytes shifted out
       // of the register unchanged, the rest through the ordinary M32 tables.
       const uint32_t zz = (uint32_t)z;
-      reg = op(0, zz ? y[0] << (8 * zz) : y[0]) ^ (zz ? y[0] >> (32 - 8 * zz) : 0u);
+      uint32_t yy = y[0];
+      for (uint32_t i = 0; i < u; ++i) yy = apply_op(T.inv1, yy);
+      reg = op(0, zz ? yy << (8 * zz) : yy) ^ (zz ? yy >> (32 - 8 * zz) : 0u);
     } else {
       reg = op(0, y[0]);
     }
@@ -143,6 +151,8 @@ int main() {
     for (int i = 0; i < v; ++i) r = (r >> 8) ^ T.sarwate[r & 0xff];
     bad += r != 0xFFFFFFFFu;
   }
+  // M32^-1 undoes M32.
+  for (uint32_t x : {0u, 1u, 0x80000000u, 0xDEADBEEFu, 0x12345678u, 0xFFFFFFFFu}) bad += apply_op(T.inv1, op(0, x)) != x;
   if (bad) { printf("table mismatch %d\n", bad); return 1; }
   std::mt19937_64 g(12345);
   std::vector<uint8_t> buf(1 << 19);
@@ -155,10 +165,11 @@ int main() {
     const uint32_t want = oracle_crc32(buf.data() + s, len);
     // model<64, true>: the wave-per-packet kernel (crc32_wave_dma_kernel, 1-KiB steps);
     // model<4, true>: the 16-packet ragged kernel (crc32_ragged16_kernel, 64-B steps).
-    const uint32_t got[7] = {model<2>(buf.data(), s, len), model<4>(buf.data(), s, len),
+    // model<8, true, true>: the 8-lane ragged kernel with 16-B-aligned chunks.
+    const uint32_t got[8] = {model<2>(buf.data(), s, len), model<4>(buf.data(), s, len),
                              model<8>(buf.data(), s, len), model<16>(buf.data(), s, len),
                              model<8, true>(buf.data(), s, len), model<64, true>(buf.data(), s, len),
-                             model<4, true>(buf.data(), s, len)};
+                             model<4, true>(buf.data(), s, len), model<8, true, true>(buf.data(), s, len)};
     for (uint32_t v : got) {
       if (v != want) {
         if (bad < 10) printf("mismatch s=%llu len=%llu want %08x got %08x\n", (unsigned long long)s,

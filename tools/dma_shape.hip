@@ -9,6 +9,9 @@
 //   16x128x2 d2  16 packets per round loaded as two 8x128 instructions, ring of 2
 //   16x128x2 d3  the same, ring of 3
 //   8x128x1 d2   the 8-lane shape with a ring of 2
+//   4x256x1 d2/3 16 lanes per packet (256-B pieces of 4 packets)
+//   2x512x1 d2   32 lanes per packet
+//   16x128x2 d1  two 8x128 instructions per slot, one slot in flight
 // Workgroups of 1024 threads, one per CU (the LDS is padded to the kernels' 150 KiB), a
 // persistent grid over static rounds.  Alternating blocks of 20 launches per shape after a
 // warm-up; prints us per launch and GB/s.  Addresses stay inside the buffer: the packets
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32
   }
   uint32_t pos = 0;
   for (uint64_t q = 0; q < q_end; ++q) {
-    acc ^= read_landed<(D - 1) * I + (I - 1)>(ring_addr(pos, 0) + 16 * lane);
+    acc ^= read_landed<(D - 1) * I>(ring_addr(pos, 0) + 16 * lane);  // both instructions of the slot
 #pragma unroll
     for (int i = 1; i < I; ++i) acc ^= read_lds(ring_addr(pos, i) + 16 * lane);
 #pragma unroll
@@ -130,12 +133,14 @@ int main(int argc, char** argv) {
   const uint32_t off = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
   // align=16: every 16-B lane load rounded down to a 16-B boundary (same pattern otherwise)
   const uint64_t amask = argc > 4 && atoi(argv[4]) == 16 ? ~(uint64_t)15 : ~(uint64_t)0;
-  n -= n % 16;
+  n -= n % 16;  // whole rounds for every shape
   if (L < 16 || L > 65536 || off > 64) return 1;
   const Shape shapes[] = {
       {"8x128x1 d3", 8, launch_shape<8, 128, 1, 3>},   {"16x64x1 d3", 16, launch_shape<16, 64, 1, 3>},
       {"16x128x2 d2", 16, launch_shape<16, 128, 2, 2>}, {"16x128x2 d3", 16, launch_shape<16, 128, 2, 3>},
-      {"8x128x1 d2", 8, launch_shape<8, 128, 1, 2>},
+      {"8x128x1 d2", 8, launch_shape<8, 128, 1, 2>},   {"4x256x1 d2", 4, launch_shape<4, 256, 1, 2>},
+      {"4x256x1 d3", 4, launch_shape<4, 256, 1, 3>},   {"2x512x1 d2", 2, launch_shape<2, 512, 1, 2>},
+      {"16x128x2 d1", 16, launch_shape<16, 128, 2, 1>},
   };
   const int ns = sizeof(shapes) / sizeof(shapes[0]);
   hipDeviceProp_t prop;
