@@ -631,7 +631,7 @@ __device__ __forceinline__ RaggedRecord ragged_record(uint64_t sa, uint32_t len,
 // aligned.  A chunk then never leaves the 16-B blocks holding packet bytes (no fallback: near
 // is 0), and the round end takes the register back over the u words with M32^-1.
 constexpr int kRecUShift = 62;
-__device__ __forceinline__ RaggedRecord ragged_record_a16(uint64_t sa, uint32_t len) {
+[[maybe_unused]] __device__ __forceinline__ RaggedRecord ragged_record_a16(uint64_t sa, uint32_t len) {
   const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
   const uint64_t a1x = sa + len + z, a1 = len ? (a1x + 15u) & ~(uint64_t)15 : a1x;
   const uint64_t top = sa & ~(uint64_t)3;
@@ -2724,8 +2724,11 @@ struct JobSlotW {
   uint32_t hist[16];           // job build: packets per class, then each class's first position
   uint32_t res[kJobPacketsW];
 };
+template <bool kDual>
 struct RaggedWLds {
-  uint32_t tables[kRepDwords + 2 * 1024];  // replicated M32^16 | M32^1 block, then M32^4 and M32^8
+  // kDual: replicated M32^32 | M32^1 block, then M32^4, M32^8, M32^16 (fill_lds); else the
+  // replicated M32^16 | M32^1 block, then M32^4 and M32^8 (fill_lds4).
+  uint32_t tables[kDual ? kLdsDwords : kRepDwords + 2 * 1024];
   u32x4 ring[kRingW][2][kWavesPerBlock][64];
   JobSlotW job[kJobSlotsW];
   uint32_t ready[kJobSlotsW];     // k + 1 once the workgroup's k-th job has its records here
@@ -2735,7 +2738,7 @@ struct RaggedWLds {
   uint32_t next_dispatch;
   uint32_t failed;                // != 0 once a wave gave up a wait (report_fault)
 };
-static_assert(sizeof(RaggedWLds) <= 160 * 1024, "LDS");
+static_assert(sizeof(RaggedWLds<false>) <= 160 * 1024 && sizeof(RaggedWLds<true>) <= 160 * 1024, "LDS");
 
 // A lane's plan for one round: the sources of its two DMAs per slot (packets lane / 8 and
 // 8 + lane / 8, chunk lane % 8) and the state of its two Horner chunks (packet lane / 4,
@@ -2757,7 +2760,7 @@ struct RoundW {
 };
 
 // Source of instruction i's slot-s DMA (the zero chunk before the packet's top).
-__device__ __forceinline__ uint64_t srcw(const RoundW& r, int i, int32_t s, uint64_t dummy) {
+[[maybe_unused]] __device__ __forceinline__ uint64_t srcw(const RoundW& r, int i, int32_t s, uint64_t dummy) {
   const uint64_t cb = i ? r.cb1 : r.cb0;
   const int32_t top = i ? r.top1 : r.top0;
   const bool real = s > top || (s == top && ((r.direct >> i) & 1u));
@@ -2783,7 +2786,7 @@ __device__ __forceinline__ void dma_plan_w(uint64_t ax, uint32_t info, bool vali
 }
 
 // A lane's round plan from the three records it reads and the round header.
-__device__ __forceinline__ RoundW roundw_from_records(uint64_t axc, uint32_t ic, uint64_t ax0, uint32_t i0,
+[[maybe_unused]] __device__ __forceinline__ RoundW roundw_from_records(uint64_t axc, uint32_t ic, uint64_t ax0, uint32_t i0,
                                                       uint64_t ax1, uint32_t i1, bool rv, uint32_t hdr,
                                                       const LaneConsts& c) {
   const uint32_t lane = threadIdx.x & 63u, kc = lane & 3u, k8 = lane & 7u;
@@ -2863,7 +2866,7 @@ __device__ __forceinline__ void read_landed2(uint32_t addr_hi, uint32_t addr_lo,
 }
 
 // h <- M(h) ^ w with the 16 lookups in one asm statement (no ring read).
-__device__ __forceinline__ void horner_step_lds(const Lookup& lk, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+[[maybe_unused]] __device__ __forceinline__ void horner_step_lds(const Lookup& lk, uint32_t& h0, uint32_t& h1, uint32_t& h2,
                                                 uint32_t& h3, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   uint32_t a[16];
   const uint32_t hs[4] = {h0, h1, h2, h3};
@@ -2930,8 +2933,69 @@ __device__ __forceinline__ void horner_step_and_read2(const Lookup& lk, uint32_t
       : "memory");
 }
 
+// A lane's Horner state: stream a (chunk kc of every 128-B piece) and, in the dual-stream
+// form, stream b (chunk kc + 4).  The single-stream form runs one M32^16 stream through
+// both chunks (b unused).
+struct HState {
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+};
+
+// Dual-stream slot: a <- M32^32(a) ^ wa and b <- M32^32(b) ^ wb, the 32 lookups of both in
+// one LDS round trip, fused with the next slot's two ring reads (vmcnt(N) before them).
+template <int N>
+__device__ __forceinline__ void horner2_step_and_read2(const Lookup& lk, HState& h, uint32_t wa0, uint32_t wa1,
+                                                       uint32_t wa2, uint32_t wa3, uint32_t wb0, uint32_t wb1,
+                                                       uint32_t wb2, uint32_t wb3, uint32_t addr_hi, uint32_t addr_lo,
+                                                       u32x4& nhi, u32x4& nlo) {
+  uint32_t a[32];
+  const uint32_t hs[8] = {h.a0, h.a1, h.a2, h.a3, h.b0, h.b1, h.b2, h.b3};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[4 * j + t] = lookup_addr(hs[j], lk.lp, lk, t);
+  }
+  asm volatile(
+      "ds_read_b32 %10, %10\n\tds_read_b32 %11, %11\n\tds_read_b32 %12, %12\n\tds_read_b32 %13, %13\n\t"
+      "ds_read_b32 %14, %14\n\tds_read_b32 %15, %15\n\tds_read_b32 %16, %16\n\tds_read_b32 %17, %17\n\t"
+      "ds_read_b32 %18, %18\n\tds_read_b32 %19, %19\n\tds_read_b32 %20, %20\n\tds_read_b32 %21, %21\n\t"
+      "ds_read_b32 %22, %22\n\tds_read_b32 %23, %23\n\tds_read_b32 %24, %24\n\tds_read_b32 %25, %25\n\t"
+      "ds_read_b32 %26, %26\n\tds_read_b32 %27, %27\n\tds_read_b32 %28, %28\n\tds_read_b32 %29, %29\n\t"
+      "ds_read_b32 %30, %30\n\tds_read_b32 %31, %31\n\tds_read_b32 %32, %32\n\tds_read_b32 %33, %33\n\t"
+      "ds_read_b32 %34, %34\n\tds_read_b32 %35, %35\n\tds_read_b32 %36, %36\n\tds_read_b32 %37, %37\n\t"
+      "ds_read_b32 %38, %38\n\tds_read_b32 %39, %39\n\tds_read_b32 %40, %40\n\tds_read_b32 %41, %41\n\t"
+      "s_waitcnt vmcnt(%52)\n\t"
+      "ds_read_b128 %8, %42\n\t"
+      "ds_read_b128 %9, %43\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_bitop3_b32 %10, %10, %11, %12 bitop3:0x96\n\t"
+      "v_bitop3_b32 %0, %10, %13, %44 bitop3:0x96\n\t"
+      "v_bitop3_b32 %14, %14, %15, %16 bitop3:0x96\n\t"
+      "v_bitop3_b32 %1, %14, %17, %45 bitop3:0x96\n\t"
+      "v_bitop3_b32 %18, %18, %19, %20 bitop3:0x96\n\t"
+      "v_bitop3_b32 %2, %18, %21, %46 bitop3:0x96\n\t"
+      "v_bitop3_b32 %22, %22, %23, %24 bitop3:0x96\n\t"
+      "v_bitop3_b32 %3, %22, %25, %47 bitop3:0x96\n\t"
+      "v_bitop3_b32 %26, %26, %27, %28 bitop3:0x96\n\t"
+      "v_bitop3_b32 %4, %26, %29, %48 bitop3:0x96\n\t"
+      "v_bitop3_b32 %30, %30, %31, %32 bitop3:0x96\n\t"
+      "v_bitop3_b32 %5, %30, %33, %49 bitop3:0x96\n\t"
+      "v_bitop3_b32 %34, %34, %35, %36 bitop3:0x96\n\t"
+      "v_bitop3_b32 %6, %34, %37, %50 bitop3:0x96\n\t"
+      "v_bitop3_b32 %38, %38, %39, %40 bitop3:0x96\n\t"
+      "v_bitop3_b32 %7, %38, %41, %51 bitop3:0x96"
+      : "=&v"(h.a0), "=&v"(h.a1), "=&v"(h.a2), "=&v"(h.a3), "=&v"(h.b0), "=&v"(h.b1), "=&v"(h.b2), "=&v"(h.b3),
+        "=&v"(nhi), "=&v"(nlo), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
+        "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]),
+        "+v"(a[15]), "+v"(a[16]), "+v"(a[17]), "+v"(a[18]), "+v"(a[19]), "+v"(a[20]), "+v"(a[21]), "+v"(a[22]),
+        "+v"(a[23]), "+v"(a[24]), "+v"(a[25]), "+v"(a[26]), "+v"(a[27]), "+v"(a[28]), "+v"(a[29]), "+v"(a[30]),
+        "+v"(a[31])
+      : "v"(addr_hi), "v"(addr_lo), "v"(wa0), "v"(wa1), "v"(wa2), "v"(wa3), "v"(wb0), "v"(wb1), "v"(wb2), "v"(wb3),
+        "i"(N)
+      : "memory");
+}
+
 // The lane's top chunk (kc + 4 if kMetaTopHi, else kc) through its masks.
-__device__ __forceinline__ void mask_top_w(uint32_t meta, const TopMasks& m, uint32_t& x0, uint32_t& x1,
+[[maybe_unused]] __device__ __forceinline__ void mask_top_w(uint32_t meta, const TopMasks& m, uint32_t& x0, uint32_t& x1,
                                            uint32_t& x2, uint32_t& x3, uint32_t& y0, uint32_t& y1, uint32_t& y2,
                                            uint32_t& y3) {
   if (meta & kMetaTopHi) {
@@ -2952,10 +3016,9 @@ __device__ __forceinline__ void mask_top_w(uint32_t meta, const TopMasks& m, uin
 // below chunk kc in the packet), the second fused with the next slot's ring reads.  Lane
 // tops lie in slots B .. B + spread <= 1, issued by the previous round with per-lane
 // sources; slot B starts every stream (a stream is zero before its lane's top).
-template <int S, int NS, int B>
+template <int S, int NS, int B, bool kDual>
 __device__ __forceinline__ void roundw_slot(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                            const TopMasks& m, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                            uint32_t& h3) {
+                                            const TopMasks& m, HState& h) {
   constexpr int kF = S + kRingW;
   const u32x4 vh = R.next_hi, vl = R.next_lo;
   const uint32_t dst = R.at<S>();
@@ -2978,40 +3041,57 @@ __device__ __forceinline__ void roundw_slot(const RoundW& cur, const RoundW& nxt
         if (cur.top_slot == S) mask_top_w(cur.meta, m, x0, x1, x2, x3, y0, y1, y2, y3);
       }
     }
-    if constexpr (S == B) {
-      h0 = x0;  // M32^16(0) = 0: no lookups
-      h1 = x1;
-      h2 = x2;
-      h3 = x3;
+    if constexpr (kDual) {
+      if constexpr (S == B) {  // M32^32(0) = 0: no lookups
+        h.a0 = y0;
+        h.a1 = y1;
+        h.a2 = y2;
+        h.a3 = y3;
+        h.b0 = x0;
+        h.b1 = x1;
+        h.b2 = x2;
+        h.b3 = x3;
+        read_landed2<2 * (kRingW - 1)>(nb + R.off_hi, nb + R.off_lo, R.next_hi, R.next_lo);
+      } else {
+        horner2_step_and_read2<2 * (kRingW - 1)>(c.lk, h, y0, y1, y2, y3, x0, x1, x2, x3, nb + R.off_hi,
+                                                 nb + R.off_lo, R.next_hi, R.next_lo);
+      }
     } else {
-      horner_step_lds(c.lk, h0, h1, h2, h3, x0, x1, x2, x3);
+      if constexpr (S == B) {
+        h.a0 = x0;  // M32^16(0) = 0: no lookups
+        h.a1 = x1;
+        h.a2 = x2;
+        h.a3 = x3;
+      } else {
+        horner_step_lds(c.lk, h.a0, h.a1, h.a2, h.a3, x0, x1, x2, x3);
+      }
+      horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h.a0, h.a1, h.a2, h.a3, y0, y1, y2, y3, nb + R.off_hi,
+                                              nb + R.off_lo, R.next_hi, R.next_lo);
     }
-    horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h0, h1, h2, h3, y0, y1, y2, y3, nb + R.off_hi, nb + R.off_lo,
-                                            R.next_hi, R.next_lo);
   }
   issue_order_fence();
 }
 
-template <int NS, int B, int... S>
+template <int NS, int B, bool kDual, int... S>
 __device__ __forceinline__ void roundw_slots(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                             const TopMasks& m, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                             uint32_t& h3, std::integer_sequence<int, S...>) {
-  (roundw_slot<S, NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3), ...);
+                                             const TopMasks& m, HState& h, std::integer_sequence<int, S...>) {
+  (roundw_slot<S, NS, B, kDual>(cur, nxt, R, c, m, h), ...);
 }
 
-template <int NS, int B>
+template <int NS, int B, bool kDual>
 __device__ __forceinline__ void roundw_fast(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                            uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+                                            HState& h) {
   static_assert(B == 0 || NS == kRingW, "leading consumed slots only in ring-length rounds");
   const TopMasks m = top_masks(cur.meta);
-  roundw_slots<NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3, std::make_integer_sequence<int, NS>{});
+  roundw_slots<NS, B, kDual>(cur, nxt, R, c, m, h, std::make_integer_sequence<int, NS>{});
   R.rotate((uint32_t)(NS % 2));
 }
 
 // Any round (wider spreads, longer packets, chunks below the caller's buffer, a job's
 // partial last round): per-lane top slots and sources, runtime slot count.
+template <bool kDual>
 __device__ __forceinline__ void roundw_generic(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                               uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+                                               HState& h) {
   const TopMasks tm = top_masks(cur.meta);
   uint32_t m = 0;  // s % 2
   for (int32_t s = 0; s < cur.ns; ++s) {
@@ -3042,33 +3122,57 @@ __device__ __forceinline__ void roundw_generic(const RoundW& cur, const RoundW& 
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
       if (top) mask_top_w(cur.meta, tm, x0, x1, x2, x3, y0, y1, y2, y3);
     }
-    horner_step_lds(c.lk, h0, h1, h2, h3, x0, x1, x2, x3);
     const uint32_t nb = R.at_rt(m);
-    horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h0, h1, h2, h3, y0, y1, y2, y3, nb + R.off_hi, nb + R.off_lo,
-                                            R.next_hi, R.next_lo);
+    if constexpr (kDual) {
+      horner2_step_and_read2<2 * (kRingW - 1)>(c.lk, h, y0, y1, y2, y3, x0, x1, x2, x3, nb + R.off_hi, nb + R.off_lo,
+                                               R.next_hi, R.next_lo);
+    } else {
+      horner_step_lds(c.lk, h.a0, h.a1, h.a2, h.a3, x0, x1, x2, x3);
+      horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h.a0, h.a1, h.a2, h.a3, y0, y1, y2, y3, nb + R.off_hi,
+                                              nb + R.off_lo, R.next_hi, R.next_lo);
+    }
     issue_order_fence();
   }
   R.rotate(m);
 }
 
-template <int... I>
+template <bool kDual, int... I>
 __device__ __forceinline__ bool roundw_dispatch(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                                uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3,
-                                                std::integer_sequence<int, I...>) {
+                                                HState& h, std::integer_sequence<int, I...>) {
   if (cur.ns == kRingW) {
-    if (cur.B == 0) roundw_fast<kRingW, 0>(cur, nxt, R, c, h0, h1, h2, h3);
-    else if (cur.B == 1) roundw_fast<kRingW, 1>(cur, nxt, R, c, h0, h1, h2, h3);
+    if (cur.B == 0) roundw_fast<kRingW, 0, kDual>(cur, nxt, R, c, h);
+    else if (cur.B == 1) roundw_fast<kRingW, 1, kDual>(cur, nxt, R, c, h);
     else return false;
     return true;
   }
-  return ((cur.ns == I + kRingW + 1 ? (roundw_fast<I + kRingW + 1, 0>(cur, nxt, R, c, h0, h1, h2, h3), true)
-                                    : false) ||
+  return ((cur.ns == I + kRingW + 1 ? (roundw_fast<I + kRingW + 1, 0, kDual>(cur, nxt, R, c, h), true) : false) ||
           ...);
 }
 
+// Dual-stream combine, valid on lane kc == 0: each stream's 4 words in-lane (M32^1), stream b
+// (chunks kc + 4: 16 words before stream a) through M32^16, then the 2-level tree M32^4, M32^8
+// across the packet's 4 lanes (fill_lds's tree tables).
+[[maybe_unused]] __device__ __forceinline__ uint32_t combine_dual(const uint32_t* lds, const HState& h, const Lookup& lk) {
+  uint32_t ya = apply_rep(lds, h.a0, h.a1, lk.lp1, lk);
+  uint32_t yb = apply_rep(lds, h.b0, h.b1, lk.lp1, lk);
+  ya = apply_rep(lds, ya, h.a2, lk.lp1, lk);
+  yb = apply_rep(lds, yb, h.b2, lk.lp1, lk);
+  ya = apply_rep(lds, ya, h.a3, lk.lp1, lk);
+  yb = apply_rep(lds, yb, h.b3, lk.lp1, lk);
+  uint32_t y = ya ^ apply_small(lds + kTreeDword + 2048, yb);
+  const uint32_t k = threadIdx.x & (kG4 - 1);
+  uint32_t t = 0;
+  if (k & 1u) t = apply_small(lds + kTreeDword, y);
+  y ^= from_lane_plus<1>(t);
+  if (k == 2u) t = apply_small(lds + kTreeDword + 1024, y);
+  y ^= from_lane_plus<2>(t);
+  return y;
+}
+
+template <bool kDual>
 __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16w_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
   send_servers_home();
-  __shared__ __attribute__((aligned(16))) RaggedWLds S;
+  __shared__ __attribute__((aligned(16))) RaggedWLds<kDual> S;
   uint32_t* const lds = S.tables;
   constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
   if (threadIdx.x < (unsigned)kJobSlotsW) {
@@ -3081,7 +3185,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16
     S.next_dispatch = kWavesPerBlock * kLook;
     S.failed = 0;
   }
-  fill_lds4(lds);
+  if constexpr (kDual)
+    fill_lds(lds);
+  else
+    fill_lds4(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -3264,11 +3371,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16
         job_dma(job_of(kb), bslot);
       }
     }
-    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    if (!cur.fast || !roundw_dispatch(cur, nxt, R, c, h0, h1, h2, h3,
-                                      std::make_integer_sequence<int, kFastWMax - kRingW>{}))
-      roundw_generic(cur, nxt, R, c, h0, h1, h2, h3);
-    const uint32_t y = combine_tree4(lds, h0, h1, h2, h3, c.lk);
+    HState h = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!cur.fast || !roundw_dispatch<kDual>(cur, nxt, R, c, h, std::make_integer_sequence<int, kFastWMax - kRingW>{}))
+      roundw_generic<kDual>(cur, nxt, R, c, h);
+    uint32_t y;
+    if constexpr (kDual)
+      y = combine_dual(lds, h, c.lk);
+    else
+      y = combine_tree4(lds, h.a0, h.a1, h.a2, h.a3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane kc == 0 holds it
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
     const uint32_t k0 = cur.job_k, slot0 = k0 & (uint32_t)(kJobSlotsW - 1);
@@ -3494,7 +3604,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
   // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
   // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
-#if defined(ENET_CRC_RAGGED16W)  // fixed jobs of 16 rounds (the kernel's d >> 4)
+#if defined(ENET_CRC_RAGGED16W) || defined(ENET_CRC_RAGGED16D)  // fixed jobs of 16 rounds (the kernel's d >> 4)
   constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRoundsW, kMinJobRounds = kJobRoundsW;
 #elif defined(ENET_CRC_RAGGED16)
   constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRounds4, kMinJobRounds = kJobRounds4 / 2;
@@ -3534,8 +3644,10 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
   jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
 #endif
-#if defined(ENET_CRC_RAGGED16W)
-  hipLaunchKernelGGL(crc32_ragged16w_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+#if defined(ENET_CRC_RAGGED16D)
+  hipLaunchKernelGGL(crc32_ragged16w_kernel<true>, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
+#elif defined(ENET_CRC_RAGGED16W)
+  hipLaunchKernelGGL(crc32_ragged16w_kernel<false>, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
 #elif defined(ENET_CRC_RAGGED16)
   hipLaunchKernelGGL(crc32_ragged16_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
 #else
