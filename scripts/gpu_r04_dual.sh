@@ -11,3 +11,4 @@ ENET_CRC_AMD_LIB=$GRAFT_REPO_ROOT/$D timeout -k 10 600 python -u -m pytest tests
 tail -1 $O/pytest_gpu_dual.log
 timeout -k 10 300 python -u scripts/ab_ragged.py $D $P --configs g2,frag,r740,r1396 > $O/ab_dual.txt 2>&1 || { cat $O/ab_dual.txt; exit 1; }
 grep -v amdgpu.ids $O/ab_dual.txt | grep -v '^{'
+bash scripts/gpu_r04_g1shape.sh ${1:-r04_dual} || exit $?

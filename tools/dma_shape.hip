@@ -17,7 +17,7 @@
 // warm-up; prints us per launch and GB/s.  Addresses stay inside the buffer: the packets
 // start 4 KiB into the allocation and a chunk never reaches more than 128 B before a packet.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/dma_shape tools/dma_shape.hip
-//   tools/dma_shape [L=1392] [packets=1605632] [base_offset=0] [align: 16 rounds every lane load down to 16 B]
+//   tools/dma_shape [L=1392] [packets=1605632] [base_offset=0] [align=1: piece starts rounded down to this]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32
     const uint32_t t = ns - 1 - s;
     const uint32_t pkt = i * (64 / kLanesPerPkt) + lane / kLanesPerPkt, k = lane % kLanesPerPkt;
     const uint8_t* end = base + (r * P + pkt + 1) * (uint64_t)L;
-    return (const uint8_t*)((uint64_t)(end - (uint64_t)PIECE * (t + 1) + 16 * k) & amask);
+    return (const uint8_t*)(((uint64_t)(end - (uint64_t)PIECE * (t + 1)) & amask) + 16 * k);
   };
   uint64_t dj = 0;
   uint32_t dsl = 0;
@@ -131,8 +131,11 @@ int main(int argc, char** argv) {
   const uint32_t L = argc > 1 ? (uint32_t)atoi(argv[1]) : 1392;
   uint64_t n = argc > 2 ? strtoull(argv[2], nullptr, 10) : 1605632;
   const uint32_t off = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
-  // align=16: every 16-B lane load rounded down to a 16-B boundary (same pattern otherwise)
-  const uint64_t amask = argc > 4 && atoi(argv[4]) == 16 ? ~(uint64_t)15 : ~(uint64_t)0;
+  // align=A (a power of two): every piece's start rounded down to an A-byte boundary (16: the
+  // lane loads 16-B aligned; 128 with 128-B pieces: whole lines, the G1 kernel's loads)
+  const uint64_t align = argc > 4 ? (uint64_t)atoi(argv[4]) : 1;
+  if (align == 0 || (align & (align - 1)) || align > 1024) return 1;
+  const uint64_t amask = ~(align - 1);
   n -= n % 16;  // whole rounds for every shape
   if (L < 16 || L > 65536 || off > 64) return 1;
   const Shape shapes[] = {
@@ -152,12 +155,12 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&buf, bytes + 8192));
   CHECK(hipMalloc(&out, (size_t)grid * 1024 * 4));
   CHECK(hipMemset(buf, 0x5a, bytes + 8192));
-  const uint8_t* base = buf + 4096 + off;
+  const uint8_t* base = buf + 4096 + off;  // pieces rounded down by up to 1023 B stay inside the allocation
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  printf("L=%u packets=%llu bytes=%llu base_offset=%u align=%s grid=%d\n", L, (unsigned long long)n,
-         (unsigned long long)bytes, off, amask == ~(uint64_t)0 ? "none" : "16", grid);
+  printf("L=%u packets=%llu bytes=%llu base_offset=%u align=%llu grid=%d\n", L, (unsigned long long)n,
+         (unsigned long long)bytes, off, (unsigned long long)align, grid);
   // warm-up through the power-management transient
   for (int w = 0; w < 60; ++w) shapes[w % ns].launch(grid, base, L, n / shapes[w % ns].P, amask, out);
   CHECK(hipGetLastError());
