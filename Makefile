@@ -46,7 +46,7 @@ $(ORACLE_RANGE): oracle/range_coder_oracle.c
 
 # A/B builds of the library with compile-time variant switches (never the product):
 #   make variant NAME=nolines DEFS=-DENET_CRC_NO_LINES
-#   -> rusty_enet_amd/lib/variants/libenet_crc_amd_region.so, loaded with ENET_CRC_AMD_LIB.
+#   -> rusty_enet_amd/lib/variants/libenet_crc_amd_nolines.so, loaded with ENET_CRC_AMD_LIB.
 variant: $(HIP_DEP)
 	mkdir -p rusty_enet_amd/lib/variants
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o rusty_enet_amd/lib/variants/libenet_crc_amd_$(NAME).so $(HIP_SRC)

@@ -328,6 +328,39 @@ __device__ __forceinline__ uint32_t combine_tree(const uint32_t* lds, uint32_t h
   return y;
 }
 
+// Two independent combine_tree chains, level by level (both rounds' lookups in flight together).
+[[maybe_unused]] __device__ __forceinline__ void combine_tree2(const uint32_t* lds, uint32_t a0, uint32_t a1,
+                                                               uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
+                                                               uint32_t b2, uint32_t b3, const Lookup& lk, uint32_t& ya,
+                                                               uint32_t& yb) {
+  ya = apply_rep(lds, a0, a1, lk.lp1, lk);
+  yb = apply_rep(lds, b0, b1, lk.lp1, lk);
+  ya = apply_rep(lds, ya, a2, lk.lp1, lk);
+  yb = apply_rep(lds, yb, b2, lk.lp1, lk);
+  ya = apply_rep(lds, ya, a3, lk.lp1, lk);
+  yb = apply_rep(lds, yb, b3, lk.lp1, lk);
+  const uint32_t k = threadIdx.x & (G - 1);
+  uint32_t ta = 0, tb = 0;
+  if (k & 1u) {
+    ta = apply_small(lds + kTreeDword, ya);
+    tb = apply_small(lds + kTreeDword, yb);
+  }
+  ya ^= from_lane_plus<1>(ta);
+  yb ^= from_lane_plus<1>(tb);
+  if ((k & 3u) == 2u) {
+    ta = apply_small(lds + kTreeDword + 1024, ya);
+    tb = apply_small(lds + kTreeDword + 1024, yb);
+  }
+  ya ^= from_lane_plus<2>(ta);
+  yb ^= from_lane_plus<2>(tb);
+  if (k == 4u) {
+    ta = apply_small(lds + kTreeDword + 2048, ya);
+    tb = apply_small(lds + kTreeDword + 2048, yb);
+  }
+  ya ^= from_lane_plus<4>(ta);
+  yb ^= from_lane_plus<4>(tb);
+}
+
 // combine_tree for the register-ring kernel's layout (kRegsLdsDwords): the first two tree
 // levels through the replicated tree block (conflict-free), the third unreplicated.
 __device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
@@ -1974,6 +2007,48 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     return rr;
   };
 
+  // A round's checksum (lane k == 0 of each group) into its job's result array; the last
+  // round of a job writes the job's checksums to HBM.
+  auto publish = [&](uint32_t k0, uint32_t id, uint32_t meta, uint32_t job_rounds, uint32_t reg) {
+    // The round's checksums into the job's result array; the last round of a job
+    // writes the job's checksums to HBM.
+    const uint32_t slot0 = k0 % kJobSlots;
+    if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
+      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
+        seen_freed = k0 + 1u - (uint32_t)kJobSlots;
+    }
+    // The checksum store is not waited for on its own: the done counter's wait below covers
+    // it (LDS operations complete in order).
+    if (c.k == 0 && (meta & kMetaStore)) lds_st32_nowait(lds_addr(&S.job[slot0].res[id]), __builtin_bswap32(~reg));
+    uint32_t old = 0;
+    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
+    old = __builtin_amdgcn_readfirstlane(old);
+    // After a failure in the workgroup nothing more is flushed: a job whose records or
+    // result slot were skipped would leave stale checksums in res[].
+    if (old + 1u == job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
+      const uint64_t J0 = job_of(k0);
+      const uint32_t n0 = job_count(J0);
+      const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
+      uint32_t* dst = out + J0 * JP + 4u * lane;
+      if (4u * lane + 4u <= n0) {
+        reinterpret_cast<U32x4A4*>(dst)->v = v;
+      } else {
+        if (4u * lane + 0u < n0) dst[0] = v.x;
+        if (4u * lane + 1u < n0) dst[1] = v.y;
+        if (4u * lane + 2u < n0) dst[2] = v.z;
+      }
+    }
+    if (old + 1u == job_rounds) {
+      if (lane == 0) {
+        lds_st32(lds_addr(&S.done[slot0]), 0u);
+        lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
+      }
+    }
+  };
+#ifdef ENET_CRC_PAIR_COMBINE
+  bool held = false;
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, pmeta = 0, pid = 0, pk = 0, pjr = 0;
+#endif
   uint32_t rnd0 = wv, rnd1 = wv + kWavesPerBlock;
   if (!round_valid(rnd0)) return;
   RaggedRound cur = make_round(rnd0);
@@ -2025,6 +2100,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     st_body += st_b1 - st_b0;
     ++st_rounds;
 #endif
+#ifdef ENET_CRC_PAIR_COMBINE
+    // Measurement build: a round whose successor is live keeps its streams (held) and is
+    // combined together with that successor, both dependent lookup chains in flight at once.
+    if (!held && nxt.live) {
+      held = true;
+      q0 = h0;
+      q1 = h1;
+      q2 = h2;
+      q3 = h3;
+      pmeta = cur.meta;
+      pid = cur.id;
+      pk = cur.job_k;
+      pjr = cur.job_rounds;
+    } else if (held) {
+      held = false;
+      uint32_t yq, y;
+      combine_tree2(lds, q0, q1, q2, q3, h0, h1, h2, h3, c.lk, yq, y);
+      const uint32_t rq = finish_word(lds, yq, (pmeta >> kMetaNTailShift) & 3u, c.lk);
+      const uint32_t rc = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);
+      publish(pk, pid, pmeta, pjr, (pmeta & kMetaEmpty) ? kInitRegister : rq);
+      publish(cur.job_k, cur.id, cur.meta, cur.job_rounds, (cur.meta & kMetaEmpty) ? kInitRegister : rc);
+    } else
+#endif
+    {
     uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
 #ifdef ENET_CRC_RAGGED_A16
     {  // back over the u zero words past the packet: y <- M32^-u y (lane k == 0, u = 0..3)
@@ -2042,39 +2141,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     reg = __builtin_amdgcn_readfirstlane(reg) == 0x12345678u ? reg + 1u : reg;  // the combine ends here
     st_comb += __builtin_amdgcn_s_memtime() - st_b1;
 #endif
-    // The round's checksums into the job's result array; the last round of a job
-    // writes the job's checksums to HBM.
-    const uint32_t k0 = cur.job_k, slot0 = k0 % kJobSlots;
-    if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
-      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
-        seen_freed = k0 + 1u - (uint32_t)kJobSlots;
-    }
-    // The checksum store is not waited for on its own: the done counter's wait below covers
-    // it (LDS operations complete in order).
-    if (c.k == 0 && (cur.meta & kMetaStore)) lds_st32_nowait(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
-    uint32_t old = 0;
-    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
-    old = __builtin_amdgcn_readfirstlane(old);
-    // After a failure in the workgroup nothing more is flushed: a job whose records or
-    // result slot were skipped would leave stale checksums in res[].
-    if (old + 1u == cur.job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
-      const uint64_t J0 = job_of(k0);
-      const uint32_t n0 = job_count(J0);
-      const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
-      uint32_t* dst = out + J0 * JP + 4u * lane;
-      if (4u * lane + 4u <= n0) {
-        reinterpret_cast<U32x4A4*>(dst)->v = v;
-      } else {
-        if (4u * lane + 0u < n0) dst[0] = v.x;
-        if (4u * lane + 1u < n0) dst[1] = v.y;
-        if (4u * lane + 2u < n0) dst[2] = v.z;
-      }
-    }
-    if (old + 1u == cur.job_rounds) {
-      if (lane == 0) {
-        lds_st32(lds_addr(&S.done[slot0]), 0u);
-        lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
-      }
+    publish(cur.job_k, cur.id, cur.meta, cur.job_rounds, reg);
     }
 #ifdef ENET_CRC_ROUND_STAMPS
     const uint64_t st_j0 = __builtin_amdgcn_s_memtime();
