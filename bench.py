@@ -638,10 +638,15 @@ def all_ranks_point(name: str, dev, rank: int, world: int, n: int, steps: int, w
     return out
 
 
+SUSTAIN_MS = 60.0  # extra points: timed after at least this much of their own load (config_point)
+
+
 def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, barrier,
                  length: int | None = None) -> dict:
     """One more workload timed on this GPU after the main line (verified on a sample first):
-    the N = 1 line carries the other BASELINE configs' per-GPU shapes next to G1."""
+    the N = 1 line carries the other BASELINE configs' per-GPU shapes next to G1.  Timed twice:
+    `cold` right after the line's warmup, and the point's own numbers once the workload has
+    run for SUSTAIN_MS (the sustained rate a receive path under load sees)."""
     import torch
 
     step, nbytes, npk, out, spec = make_workload(name, rank, n, dev, length=length)
@@ -652,11 +657,21 @@ def config_point(name: str, dev, rank: int, n: int, steps: int, warmup: int, bar
     pre = ceil.measure(spec[1], nbytes) if ceil else None
     for _ in range(warmup):
         step()
+    wall_c, kms_c = time_steps(step, steps, barrier, dev)  # right after the line's own warmup
+    # Sustained: the ragged kernel's launches speed up over its first ~30 ms of load (power
+    # management; profiles/r04/rramp/ragged_series.txt, 193 -> 150 us), so every point is
+    # timed again after at least SUSTAIN_MS of this workload's launches.
+    extra = max(0, math.ceil(SUSTAIN_MS / max(kms_c, 1e-3)) - warmup - steps)
+    for _ in range(extra):
+        step()
     wall, kms = time_steps(step, steps, barrier, dev)
     ms = wall * 1000.0 / steps
     res = {"packets": npk, "bytes": nbytes, "ms_per_step": round(ms, 5),
            "value": round(nbytes / (ms / 1000.0) / 2**30, 2), "unit": "GiB/s",
-           "kernel_ms": round(kms, 5), "frac": round(nbytes / (kms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)}
+           "kernel_ms": round(kms, 5), "frac": round(nbytes / (kms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4),
+           "timed_after_launches": warmup + steps + extra,
+           "cold": {"kernel_ms": round(kms_c, 5), "frac": round(nbytes / (kms_c / 1000.0) / 1e9 / HBM_PEAK_GBS, 4),
+                    "ms_per_step": round(wall_c * 1000.0 / steps, 5), "timed_after_launches": warmup}}
     cf = ceiling_fields(ceil, pre, spec[1] if ceil else None, nbytes, nbytes / (kms / 1000.0) / 1e9)
     res["read_ceiling_gbs"], res["frac_of_ceiling"] = cf["read_ceiling_gbs"], cf["frac_of_ceiling"]
     if name in ("ragged", "large", "frag") and n == CONFIGS[name][1]:

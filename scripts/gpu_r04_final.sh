@@ -10,3 +10,4 @@ timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_2
 python scripts/line_summary.py $O/bench_20_5.json
 timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit $?
 python scripts/line_summary.py $O/bench_default.json
+bash scripts/gpu_r04_pair.sh ${1:-r04_final} || exit $?

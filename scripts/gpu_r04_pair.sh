@@ -11,3 +11,4 @@ ENET_CRC_AMD_LIB=$GRAFT_REPO_ROOT/$V timeout -k 10 600 python -u -m pytest tests
 tail -1 $O/pytest_gpu_pair.log
 timeout -k 10 300 python -u scripts/ab_ragged.py $V $P --configs g2,frag,r740,r1396 > $O/ab_pair.txt 2>&1 || { cat $O/ab_pair.txt; exit 1; }
 grep -v amdgpu.ids $O/ab_pair.txt | grep -v '^{'
+bash scripts/gpu_r04_rramp.sh ${1:-r04_pair} || exit $?

@@ -12,5 +12,7 @@ for path in sys.argv[1:]:
     for k in ("shard_2m", "mtu_1392", "ragged_g2", "large_64k", "frag_64k"):
         if k in line:
             p = line[k]
+            cold = p.get("cold", {}).get("kernel_ms")
             print(f"  {k:10s} kernel {p['kernel_ms'] * 1000:7.1f} us  frac {p['frac']:.4f}  "
-                  f"ceiling {p.get('read_ceiling_gbs')}  frac_of_ceiling {p.get('frac_of_ceiling')}")
+                  f"ceiling {p.get('read_ceiling_gbs')}  frac_of_ceiling {p.get('frac_of_ceiling')}"
+                  + (f"  (cold {cold * 1000:.1f} us)" if cold else ""))

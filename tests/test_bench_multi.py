@@ -74,6 +74,9 @@ def test_multi_gpu_line_shape(tmp_path):
     big = line["large_64k"]
     assert big["n_gpus"] == 2 and big["packets"] == 32768  # configs[4]: 256K over 8
     assert big["ms_per_step"] == pytest.approx(2.0) and big["kernel_ms"] == pytest.approx(1.8)
+    # timed twice: right after the warmup (cold) and after SUSTAIN_MS of the point's own launches
+    assert big["cold"]["timed_after_launches"] == 1 and big["cold"]["kernel_ms"] > 0
+    assert big["timed_after_launches"] >= 1 + 4 and big["timed_after_launches"] * 0.9 >= 60.0
     assert big["value"] == pytest.approx(2 * 32768 * 65536 / 2e-3 / 2**30, rel=1e-3)
     assert big["frac"] == pytest.approx(32768 * 65536 / 1.8e-3 / 1e9 / 8000.0, rel=1e-3)
     assert line["roofline"]["read_ceiling_gbs"] is None and "not built" in line["roofline"]["read_ceiling"]["note"]
