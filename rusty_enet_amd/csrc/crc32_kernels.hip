@@ -1556,9 +1556,19 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   // Fast: every packet starts at the same slot (same step count), no fallback chunk,
   // and the lanes whose top chunk lies before their packet are exactly the ones the
   // round reads as zeros (ragged_src with !direct).
-  rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
   const bool fallback = __builtin_amdgcn_ballot_w64(rr.meta & kMetaFallback) != 0;
+#ifdef ENET_CRC_SPREAD_FAST
+  // Measurement build: the unrolled bodies also take rounds whose packets' top slots differ
+  // (two step classes meeting in a round): every top slot in B .. B + 1 (B = ns - max steps;
+  // B .. ring - 1 in ring-length rounds, empty packets included), all inside the slots the
+  // previous round issued with per-lane sources; each lane masks its own top chunk there.
+  rr.top_uniform = rr.ns - max_steps;  // B
+  const int32_t lim = rr.ns == kRaggedRing ? kRaggedRing : rr.top_uniform + 1;
+  rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot > lim) && !fallback && rr.ns <= kRaggedFastMax;
+#else
+  rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
   rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform) && !fallback && rr.ns <= kRaggedFastMax;
+#endif
   return rr;
 }
 
@@ -1624,10 +1634,21 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
     }
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     if (s == NS - 1) mask_last(cur, w0, w1, w2, w3);  // data only: before the injection in mask_top
+#ifdef ENET_CRC_SPREAD_FAST
+    // each lane's own top slot (B .. B + 1, or B .. ring - 1 in ring-length rounds)
+    if (s <= (NS == kRaggedRing ? kRaggedRing - 1 : T + 1)) {
+      const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
+      if (__builtin_amdgcn_ballot_w64(mine)) {
+        if (mine) mask_top(cur.meta, w0, w1, w2, w3);
+      }
+    }
+#endif
     if (s == T) {
+#ifndef ENET_CRC_SPREAD_FAST
       if (__builtin_amdgcn_ballot_w64(cur.meta & kMetaHeadMask)) {
         if (cur.meta & kMetaHeadMask) mask_top(cur.meta, w0, w1, w2, w3);
       }
+#endif
       h0 = w0;  // top step: M32^32(0) = 0, no lookups
       h1 = w1;
       h2 = w2;

@@ -11,7 +11,7 @@ for c in uniform ragged large frag range; do
   cp "$SRC/prof_$c/run_kernel_stats.csv" "$DST/${c}_kernel_stats.csv"
   python3 scripts/pmc_summary.py "$SRC/pmc_$c" > "$DST/${c}_pmc_summary.txt" 2>&1
 done
-for f in ipc_uniform_summary.txt ipc_ragged_summary.txt ipc_frag_summary.txt traffic.json pytest_gpu.log bench_rehearsal_n2.json \
+for f in ipc_uniform_summary.txt ipc_ragged_summary.txt ipc_frag_summary.txt rdreq_uniform_summary.txt rdreq_ragged_summary.txt rdreq_frag_summary.txt traffic.json pytest_gpu.log bench_rehearsal_n2.json \
          trace_20_5.json trace_20_5_kernel_trace.csv trace_20_5_vs_line.json trace_200_10.json trace_200_10_kernel_trace.csv \
          trace_200_10_vs_line.json; do
   [ -f "$SRC/$f" ] && cp "$SRC/$f" "$DST/"

@@ -39,6 +39,14 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ
   -- python3 "$ROOT/bench.py" --config range --steps 2 --warmup 1 --cpu-seconds 0 --no-verify \
   > "$OUT/pmc_range.log" 2>&1 || exit $?
 echo "[profile] range read requests done" >&2
+# L2-to-memory read requests by size (is FETCH_SIZE x 2 right for the ragged kernel's partial lines?)
+for c in uniform ragged frag; do
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
+    -d "$OUT/rdreq_$c" -o run --output-format csv \
+    -- python3 "$ROOT/bench.py" --config $c --steps 5 --warmup 1 --cpu-seconds 0 --no-verify --no-e2e --no-shard \
+    > "$OUT/rdreq_$c.log" 2>&1 || exit $?
+done
+echo "[profile] read request sizes done" >&2
 i=0
 for counters in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
                 "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
@@ -55,6 +63,7 @@ cd "$ROOT"
 python3 scripts/traffic_summary.py "gpurun_out/$TAG" > "$OUT/traffic.json" 2>&1 || exit $?
 for c in uniform ragged frag; do
   python3 scripts/pmc_summary.py "$OUT"/ipc_${c}_* > "$OUT/ipc_${c}_summary.txt" 2>&1
+  python3 scripts/pmc_summary.py "$OUT/rdreq_$c" > "$OUT/rdreq_${c}_summary.txt" 2>&1
 done
 # One bench process's per-launch kernel trace, the driver's command shape and the default
 # (the launch-time series behind the line).

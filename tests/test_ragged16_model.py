@@ -45,6 +45,11 @@ class Kernel:
 
 R16 = Kernel(lanes=4, ring=3, job_packets=512, min_rounds=16, class_long=24, max_spread=2)
 R16W = Kernel(lanes=8, ring=2, job_packets=256, min_rounds=16, class_long=14, max_spread=1)
+# crc32_ragged_jobs_kernel with ENET_CRC_SPREAD_FAST: 8 packets per round, top slots B .. B + 1
+# (any in ring-length rounds).  The model sends near-base packets to the generic body (the
+# kernel only the rounds with an actual fallback lane): it checks a subset of the fast rounds.
+R8S = Kernel(lanes=8, ring=3, job_packets=256, min_rounds=16, class_long=15, max_spread=1, packets=8)
+KERNELS = {"r16": R16, "r16w": R16W, "r8s": R8S}
 SORT_MIN = 4096
 
 
@@ -171,12 +176,12 @@ def _shape(name: str):
     return (packed_offsets(lengths) + np.cumsum(gaps)).astype(np.uint64) + np.uint64(1), lengths
 
 
-@pytest.mark.parametrize("kernel", ["r16", "r16w"])
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
 @pytest.mark.parametrize("name", ["g2", "frag", "near_base", "every_length", "wide_spread", "tiny", "long_mix",
                                   "edges", "one_job"])
 def test_ragged16_addresses(kernel, name):
     offsets, lengths = _shape(name)
-    stats = check_batch(R16 if kernel == "r16" else R16W, offsets, lengths)
+    stats = check_batch(KERNELS[kernel], offsets, lengths)
     assert stats["dmas"] > 0
     if name in ("g2", "frag", "every_length", "tiny"):
         assert stats["fast"] > stats["generic"], stats  # the sort leaves nearly all rounds fast
