@@ -1509,11 +1509,11 @@ struct RaggedRound {
   uint32_t meta;        // round_meta(); the trailing-byte field holds z (bytes run past the end)
   uint32_t id;          // packet id (output index)
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
-  bool fast;            // wave-uniform: every lane's top is the same slot, no fallback, ns <= kRaggedFastMax
+  bool fast;            // wave-uniform: top slots in B .. B + 1 (any in ring-length rounds), no fallback, ns <= kRaggedFastMax
   bool live;            // jobs kernel: the round is inside the batch (wave-uniform)
   uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
   uint32_t job_rounds;  // jobs kernel: rounds of that job
-  int32_t top_uniform;  // that slot (0 unless ns == kRaggedRing and the packets are shorter)
+  int32_t top_uniform;  // B: the first top slot of a fast round (0 unless ns == kRaggedRing)
   int32_t spread;       // 16-packet rounds: max - min step count of the round's packets (wave-uniform)
 };
 
@@ -1557,18 +1557,14 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   // and the lanes whose top chunk lies before their packet are exactly the ones the
   // round reads as zeros (ragged_src with !direct).
   const bool fallback = __builtin_amdgcn_ballot_w64(rr.meta & kMetaFallback) != 0;
-#ifdef ENET_CRC_SPREAD_FAST
-  // Measurement build: the unrolled bodies also take rounds whose packets' top slots differ
-  // (two step classes meeting in a round): every top slot in B .. B + 1 (B = ns - max steps;
-  // B .. ring - 1 in ring-length rounds, empty packets included), all inside the slots the
-  // previous round issued with per-lane sources; each lane masks its own top chunk there.
+  // Fast (unrolled body): every top slot in B .. B + 1 (B = ns - max steps; B .. ring - 1 in
+  // ring-length rounds, empty packets included), so rounds where two step classes meet take
+  // the unrolled bodies too (27 % of G2's rounds; 149.5 vs 157.8 us).  All those
+  // slots were issued by the previous round with per-lane sources, every later slot lies
+  // inside every packet, and each lane masks its own top chunk at its top slot.
   rr.top_uniform = rr.ns - max_steps;  // B
   const int32_t lim = rr.ns == kRaggedRing ? kRaggedRing : rr.top_uniform + 1;
   rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot > lim) && !fallback && rr.ns <= kRaggedFastMax;
-#else
-  rr.top_uniform = __builtin_amdgcn_readfirstlane(rr.top_slot);
-  rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot != rr.top_uniform) && !fallback && rr.ns <= kRaggedFastMax;
-#endif
   return rr;
 }
 
@@ -1612,11 +1608,12 @@ __device__ __forceinline__ void mask_last(const RaggedRound& r, uint32_t& w0, ui
 #endif
 }
 
-// A round in which every packet has the same step count and needs no fallback: the
-// slot loop of crc32_uniform_dma_kernel (unrolled, lookups fused with the next ring
-// read); slot T (the packets' top slot) masks the top words, the last slot the bytes
-// past each packet's end.  T > 0 only for rounds of packets shorter than the ring
-// (NS = kRaggedRing): their first T slots hold zero chunks and are only consumed.
+// A round whose packets' top slots lie in T .. T + 1 (T .. ring - 1 in ring-length rounds)
+// and that needs no fallback: the slot loop of crc32_uniform_dma_kernel (unrolled, lookups
+// fused with the next ring read); each lane masks its top words at its own top slot, lane
+// k == 0 the bytes past its packet's end in the last slot.  T > 0 only for rounds of packets
+// shorter than the ring (NS = kRaggedRing): their first T slots hold zero chunks and are only
+// consumed.
 template <int NS, int T = 0>
 __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
                                                   const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
@@ -1634,7 +1631,6 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
     }
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     if (s == NS - 1) mask_last(cur, w0, w1, w2, w3);  // data only: before the injection in mask_top
-#ifdef ENET_CRC_SPREAD_FAST
     // each lane's own top slot (B .. B + 1, or B .. ring - 1 in ring-length rounds)
     if (s <= (NS == kRaggedRing ? kRaggedRing - 1 : T + 1)) {
       const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
@@ -1642,14 +1638,8 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
         if (mine) mask_top(cur.meta, w0, w1, w2, w3);
       }
     }
-#endif
     if (s == T) {
-#ifndef ENET_CRC_SPREAD_FAST
-      if (__builtin_amdgcn_ballot_w64(cur.meta & kMetaHeadMask)) {
-        if (cur.meta & kMetaHeadMask) mask_top(cur.meta, w0, w1, w2, w3);
-      }
-#endif
-      h0 = w0;  // top step: M32^32(0) = 0, no lookups
+      h0 = w0;  // first top slot B: every stream is still zero (M32^32(0) = 0), no lookups
       h1 = w1;
       h2 = w2;
       h3 = w3;

@@ -1,7 +1,8 @@
-"""Host model of the 16-packet-round ragged kernels' addressing (rusty_enet_amd/csrc/
-crc32_kernels.hip): crc32_ragged16_kernel (4 lanes x 64-B pieces per packet, ring of 3) and
-crc32_ragged16w_kernel (loaded as 8 lanes x 128-B pieces per packet, two DMA instructions per
-slot, ring of 2).  Job partition, per-packet records (ragged_record4 / ragged_record), the
+"""Host model of the ragged kernels' addressing (rusty_enet_amd/csrc/crc32_kernels.hip): the
+product's crc32_ragged_jobs_kernel (8 lanes x 128-B pieces per packet, 8 packets per round,
+ring of 3), and the measurement builds crc32_ragged16_kernel (4 lanes x 64-B pieces, 16
+packets per round) and crc32_ragged16w_kernel (16 packets loaded as 8 lanes x 128-B pieces,
+two DMA instructions per slot, ring of 2).  Job partition, per-packet records (ragged_record4 / ragged_record), the
 class sort and round headers of the job build, each DMA lane's round plan
 (round16_from_record / dma_plan_w) and the source of every LDS-DMA the round bodies issue.
 No GPU.
@@ -45,11 +46,11 @@ class Kernel:
 
 R16 = Kernel(lanes=4, ring=3, job_packets=512, min_rounds=16, class_long=24, max_spread=2)
 R16W = Kernel(lanes=8, ring=2, job_packets=256, min_rounds=16, class_long=14, max_spread=1)
-# crc32_ragged_jobs_kernel with ENET_CRC_SPREAD_FAST: 8 packets per round, top slots B .. B + 1
+# crc32_ragged_jobs_kernel (the product): 8 packets per round, top slots B .. B + 1
 # (any in ring-length rounds).  The model sends near-base packets to the generic body (the
 # kernel only the rounds with an actual fallback lane): it checks a subset of the fast rounds.
-R8S = Kernel(lanes=8, ring=3, job_packets=256, min_rounds=16, class_long=15, max_spread=1, packets=8)
-KERNELS = {"r16": R16, "r16w": R16W, "r8s": R8S}
+R8 = Kernel(lanes=8, ring=3, job_packets=256, min_rounds=16, class_long=15, max_spread=1, packets=8)
+KERNELS = {"r16": R16, "r16w": R16W, "r8": R8}
 SORT_MIN = 4096
 
 
