@@ -1587,6 +1587,11 @@ struct RaggedRing {
     __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 0);
     q = q + 1 == (uint32_t)kRaggedRing ? 0u : q + 1;
   }
+  // The same with the non-temporal hint (a line read for the last time).
+  __device__ __forceinline__ void dma_nt(uint64_t src) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 2);
+    q = q + 1 == (uint32_t)kRaggedRing ? 0u : q + 1;
+  }
   __device__ __forceinline__ uint32_t next_addr() const { return ring0 + q * kRingStride + lane16; }
 };
 
@@ -1623,7 +1628,17 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
   for (int s = 0; s < NS; ++s) {
     const u32x4 v = R.nextv;
     const int32_t f = s + kRaggedRing;  // refill this slot's LDS slot kRaggedRing slots ahead
+#ifdef ENET_CRC_RAGGED_NT
+    // Measurement build: the slots past every top slot stream non-temporal, so the lines
+    // read at the top slots (shared with the previous packet, which reads them at its last
+    // slot about a round later) are the ones the L2 keeps.
+    if (f < NS)
+      R.dma_nt(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)f);
+    else
+      R.dma(ragged_src(nxt, f - NS, c.dummy));
+#else
     R.dma(f < NS ? cur.cb + (uint64_t)kBytesPerStep * (uint64_t)f : ragged_src(nxt, f - NS, c.dummy));
+#endif
     if (s < T) {
       R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
       issue_order_fence();

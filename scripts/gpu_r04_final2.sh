@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4 evidence on the final sources: the GPU suite, the driver's bench command, the default
+# bench, then the profile round (kernel stats, FETCH_SIZE, read sizes, counters, traces).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+T=${1:-r04_final2}
+O=gpurun_out/$T
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+tail -3 $O/pytest_gpu.log
+timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_20_5.json 2> $O/bench_20_5.err || exit $?
+python scripts/line_summary.py $O/bench_20_5.json
+bash scripts/gpu_profile_round.sh $T || exit $?
+python scripts/line_summary.py $O/bench_uniform.json
