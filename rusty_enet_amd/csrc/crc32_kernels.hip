@@ -3575,12 +3575,23 @@ static hipError_t dispatch_uniform_regs(int ns, const UniformBatch& u, uint32_t*
   return e;
 }
 
-// crc32_uniform_lines_kernel's batches: back to back, 16-B multiple lengths, line-aligned base.
-static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length) {
+// crc32_uniform_lines_kernel's batches: back to back, 16-B multiple lengths, from a 16-B
+// aligned base.  `head` = the packets before the first one that starts on a 128-B line (0 for
+// a line-aligned base; < 8, since L * h mod 128 runs through its residues within 128 /
+// gcd(L, 128) <= 8 steps): they go through the register ring, the whole-line kernel starts
+// at packet head.  False when no packet starts on a line (e.g. L = 1200 from base + 8).
+static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length, uint64_t& head) {
 #ifdef ENET_CRC_NO_LINES  // A/B build: the register ring for these batches too
   return false;
 #endif
-  return stride == length && (length & 15u) == 0 && (base & 127u) == 0;
+  if (stride != length || (length & 15u) != 0 || (base & 15u) != 0) return false;
+  for (uint64_t h = 0; h < (uint64_t)kPacketsPerWave; ++h) {
+    if (((base + h * length) & 127u) == 0) {
+      head = h;
+      return true;
+    }
+  }
+  return false;
 }
 
 template <int NSL>
@@ -3634,22 +3645,33 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
       return hipGetLastError();
     }
     if (nsx <= kMaxRoundSteps) {
-      // Back-to-back 16-B-multiple packets from a line-aligned base: every line read once,
-      // whole, non-temporal (crc32_uniform_lines_kernel) for the whole rounds, the register
-      // ring for the < 8 packets left.
+      // Back-to-back 16-B-multiple packets from a 16-B aligned base: every line read once,
+      // whole, non-temporal (crc32_uniform_lines_kernel) for the whole rounds from the first
+      // packet on a line, the register ring for the < 8 packets before it and after the last
+      // whole round.
       const int nsl = (int)((length + 127u) / 128u);
-      const uint64_t whole = count / kPacketsPerWave * kPacketsPerWave;
-      if (lines_shape(b0, stride, length) && nsl >= kUniformRing && nsl <= kMaxRoundSteps && whole > 0) {
-        const UniformBatch w{b0, stride, length, whole};
+      uint64_t head = 0;
+      const bool lines = lines_shape(b0, stride, length, head);
+      const uint64_t whole = lines && count > head ? (count - head) / kPacketsPerWave * kPacketsPerWave : 0;
+      if (lines && nsl >= kUniformRing && nsl <= kMaxRoundSteps && whole > 0) {
+        if (head > 0) {
+          const UniformBatch h{b0, stride, length, head};
+          const unsigned hblocks = grid_for(head, err);
+          if (err != hipSuccess) return err;
+          err = dispatch_uniform_regs(nsx, h, out, stream, hblocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
+          if (err != hipSuccess) return err;
+        }
+        const UniformBatch w{b0 + head * stride, stride, length, whole};
         const unsigned wblocks = grid_for(whole, err);
         if (err != hipSuccess) return err;
-        err = dispatch_uniform_lines(nsl, w, out, stream, wblocks,
+        err = dispatch_uniform_lines(nsl, w, out + head, stream, wblocks,
                                      std::make_integer_sequence<int, kMaxRoundSteps - kUniformRing + 1>{});
-        if (err != hipSuccess || whole == count) return err;
-        const UniformBatch t{b0 + whole * stride, stride, length, count - whole};
-        const unsigned tblocks = grid_for(count - whole, err);
+        const uint64_t done = head + whole;
+        if (err != hipSuccess || done == count) return err;
+        const UniformBatch t{b0 + done * stride, stride, length, count - done};
+        const unsigned tblocks = grid_for(count - done, err);
         if (err != hipSuccess) return err;
-        return dispatch_uniform_regs(nsx, t, out + whole, stream, tblocks,
+        return dispatch_uniform_regs(nsx, t, out + done, stream, tblocks,
                                      std::make_integer_sequence<int, kMaxRoundSteps>{});
       }
       return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});

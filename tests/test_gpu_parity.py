@@ -385,6 +385,22 @@ def test_uniform_whole_lines_kernel(dev, base_off):
         assert np.array_equal(got, want), (length, n, base_off, int(np.count_nonzero(got != want)))
 
 
+@pytest.mark.parametrize("base_off", [16, 48, 80, 112, 8, 1040])
+def test_uniform_whole_lines_head_peeled(dev, base_off):
+    # Back-to-back 16-B-multiple packets from a 16-B aligned base that is not line-aligned:
+    # the packets before the first one that starts on a line go through the register ring,
+    # the whole-line kernel takes the whole rounds from there (launch_uniform, lines_shape).
+    # Counts below, at and past the head, with and without a tail; 1280-B packets never
+    # start on a line from these bases, and base + 8 is not 16-B aligned (register ring).
+    for length, n in [(1200, 3), (1200, 9), (1200, 15), (1200, 4011), (1392, 2999), (528, 4100), (1040, 1111),
+                      (1280, 1000), (1792, 1501)]:
+        data = splitmix64_bytes(base_off * 3 + length + n, base_off + n * length)
+        d = to_dev(data, dev)[base_off:]
+        got = as_u32(rea.crc32_batch(d, stride=length, length=length, count=n))
+        want = _oracle.crc32_uniform(data[base_off:], length, length, n, threads=8)
+        assert np.array_equal(got, want), (length, n, base_off, int(np.count_nonzero(got != want)))
+
+
 def test_long_packets_line_ends(dev):
     # Non-temporal DMAs need every packet to end on a 128-B line: ends aligned with the
     # starts aligned (64 KiB from an aligned base) or not (65536 - 128 from base + 128),
