@@ -2202,6 +2202,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 }
 
 
+#if defined(ENET_CRC_RAGGED16) || defined(ENET_CRC_RAGGED16W) || defined(ENET_CRC_RAGGED16D)
+// The 16-packet-round kernels below exist only in their measurement builds (DESIGN.md §4:
+// all slower than crc32_ragged_jobs_kernel); the product library does not carry their code.
 // ---------------------------------------------------------------------------------
 // Ragged kernel with rounds of 16 packets, 4 lanes per packet (ENET_CRC_RAGGED16 measurement
 // build: slower than the 8-lane kernel).  Same pipeline as crc32_ragged_jobs_kernel above (jobs sorted by step
@@ -3508,6 +3511,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16
   }
   __builtin_amdgcn_s_waitcnt(0);
 }
+
+#endif  // 16-packet-round measurement builds
 
 }  // namespace
 
