@@ -1405,6 +1405,21 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
   uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
   u32x4 q[NSL];
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
+#ifdef ENET_CRC_EARLY_LOADS
+  // Measurement build: the first round's loads go out before the table fill, so their
+  // latency overlaps the fill's own table reads.
+  if (rnd0 < rounds) {
+    const uint64_t lb = lane_base(rnd0);
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      q[s] = ld(lb, s);
+      issue_order_fence();
+    }
+  }
+  fill_lds_regs(lds);
+  __syncthreads();
+  if (rnd0 >= rounds) return;
+#else
   fill_lds_regs(lds);
   __syncthreads();
   if (rnd0 >= rounds) return;
@@ -1416,6 +1431,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
       issue_order_fence();
     }
   }
+#endif
   uint32_t res = 0, j = 0;
   uint64_t res_round = 0;
   while (rnd0 < rounds) {
