@@ -328,39 +328,6 @@ __device__ __forceinline__ uint32_t combine_tree(const uint32_t* lds, uint32_t h
   return y;
 }
 
-// Two independent combine_tree chains, level by level (both rounds' lookups in flight together).
-[[maybe_unused]] __device__ __forceinline__ void combine_tree2(const uint32_t* lds, uint32_t a0, uint32_t a1,
-                                                               uint32_t a2, uint32_t a3, uint32_t b0, uint32_t b1,
-                                                               uint32_t b2, uint32_t b3, const Lookup& lk, uint32_t& ya,
-                                                               uint32_t& yb) {
-  ya = apply_rep(lds, a0, a1, lk.lp1, lk);
-  yb = apply_rep(lds, b0, b1, lk.lp1, lk);
-  ya = apply_rep(lds, ya, a2, lk.lp1, lk);
-  yb = apply_rep(lds, yb, b2, lk.lp1, lk);
-  ya = apply_rep(lds, ya, a3, lk.lp1, lk);
-  yb = apply_rep(lds, yb, b3, lk.lp1, lk);
-  const uint32_t k = threadIdx.x & (G - 1);
-  uint32_t ta = 0, tb = 0;
-  if (k & 1u) {
-    ta = apply_small(lds + kTreeDword, ya);
-    tb = apply_small(lds + kTreeDword, yb);
-  }
-  ya ^= from_lane_plus<1>(ta);
-  yb ^= from_lane_plus<1>(tb);
-  if ((k & 3u) == 2u) {
-    ta = apply_small(lds + kTreeDword + 1024, ya);
-    tb = apply_small(lds + kTreeDword + 1024, yb);
-  }
-  ya ^= from_lane_plus<2>(ta);
-  yb ^= from_lane_plus<2>(tb);
-  if (k == 4u) {
-    ta = apply_small(lds + kTreeDword + 2048, ya);
-    tb = apply_small(lds + kTreeDword + 2048, yb);
-  }
-  ya ^= from_lane_plus<4>(ta);
-  yb ^= from_lane_plus<4>(tb);
-}
-
 // combine_tree for the register-ring kernel's layout (kRegsLdsDwords): the first two tree
 // levels through the replicated tree block (conflict-free), the third unreplicated.
 __device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
@@ -655,27 +622,6 @@ __device__ __forceinline__ RaggedRecord ragged_record(uint64_t sa, uint32_t len,
          (1ull << kRecValidBit);
   r.info = (uint32_t)g.nsteps | ((pad >> 2) << kRecPadShift);
   r.nsteps = (uint32_t)g.nsteps;
-  return r;
-}
-
-// ragged_record with 16-B-aligned chunks (crc32_ragged_jobs_kernel under ENET_CRC_RAGGED_A16):
-// the packet runs on from a1 to the next 16-B boundary A1, u = (A1 - a1) / 4 more zero words
-// (u << kRecUShift in ax), so that every chunk address A1 - 16 (k + 1) - 128 i is 16-B
-// aligned.  A chunk then never leaves the 16-B blocks holding packet bytes (no fallback: near
-// is 0), and the round end takes the register back over the u words with M32^-1.
-constexpr int kRecUShift = 62;
-[[maybe_unused]] __device__ __forceinline__ RaggedRecord ragged_record_a16(uint64_t sa, uint32_t len) {
-  const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
-  const uint64_t a1x = sa + len + z, a1 = len ? (a1x + 15u) & ~(uint64_t)15 : a1x;
-  const uint64_t top = sa & ~(uint64_t)3;
-  const uint32_t nwords = (uint32_t)((a1 - top) >> 2);
-  const uint32_t nsteps = (nwords + 31u) >> 5;
-  const uint32_t pad = 128u * nsteps - 4u * nwords;  // 0..124
-  RaggedRecord r;
-  r.ax = a1 | ((sa & 3u) << kRecVShift) | ((uint64_t)z << kRecZShift) | (1ull << kRecValidBit) |
-         ((a1 - a1x) >> 2) << kRecUShift;
-  r.info = nsteps | ((pad >> 2) << kRecPadShift);
-  r.nsteps = nsteps;
   return r;
 }
 
@@ -1405,21 +1351,6 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
   uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
   u32x4 q[NSL];
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
-#ifdef ENET_CRC_EARLY_LOADS
-  // Measurement build: the first round's loads go out before the table fill, so their
-  // latency overlaps the fill's own table reads.
-  if (rnd0 < rounds) {
-    const uint64_t lb = lane_base(rnd0);
-#pragma unroll
-    for (int s = 0; s < NSL; ++s) {
-      q[s] = ld(lb, s);
-      issue_order_fence();
-    }
-  }
-  fill_lds_regs(lds);
-  __syncthreads();
-  if (rnd0 >= rounds) return;
-#else
   fill_lds_regs(lds);
   __syncthreads();
   if (rnd0 >= rounds) return;
@@ -1431,7 +1362,6 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
       issue_order_fence();
     }
   }
-#endif
   uint32_t res = 0, j = 0;
   uint64_t res_round = 0;
   while (rnd0 < rounds) {
@@ -1530,7 +1460,6 @@ struct RaggedRound {
   uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
   uint32_t job_rounds;  // jobs kernel: rounds of that job
   int32_t top_uniform;  // B: the first top slot of a fast round (0 unless ns == kRaggedRing)
-  int32_t spread;       // 16-packet rounds: max - min step count of the round's packets (wave-uniform)
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
@@ -1563,11 +1492,6 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
             (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
   rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
-#ifdef ENET_CRC_RAGGED_A16
-  // The zero words past the packet (16-B-aligned chunks): lane k == 0 masks them off in the
-  // last slot (mask_last) and takes the register back over them (back_over_padding).
-  if (valid && c.k == 0) rr.meta |= (uint32_t)(ax >> kRecUShift) << kMetaTShiftShift;
-#endif
   rr.id = id;
   // Fast: every packet starts at the same slot (same step count), no fallback chunk,
   // and the lanes whose top chunk lies before their packet are exactly the ones the
@@ -1584,12 +1508,10 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   return rr;
 }
 
-// Source of this lane's slot-s DMA in round rr (the zero chunk before its top); kStep bytes
-// per packet per slot (128: 8 lanes per packet, 64: 4 lanes).
-template <uint32_t kStep = kBytesPerStep>
+// Source of this lane's slot-s DMA in round rr (the zero chunk before its top).
 __device__ __forceinline__ uint64_t ragged_src(const RaggedRound& rr, int32_t s, uint64_t dummy) {
   const bool real = s > rr.top_slot || (s == rr.top_slot && (rr.meta & kMetaDirect));
-  return real ? rr.cb + (uint64_t)kStep * (uint64_t)s : dummy;
+  return real ? rr.cb + (uint64_t)kBytesPerStep * (uint64_t)s : dummy;
 }
 
 // Shared state of one wave's LDS-DMA ring (crc32_ragged_jobs_kernel).
@@ -1603,31 +1525,8 @@ struct RaggedRing {
     __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 0);
     q = q + 1 == (uint32_t)kRaggedRing ? 0u : q + 1;
   }
-  // The same with the non-temporal hint (a line read for the last time).
-  __device__ __forceinline__ void dma_nt(uint64_t src) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 2);
-    q = q + 1 == (uint32_t)kRaggedRing ? 0u : q + 1;
-  }
   __device__ __forceinline__ uint32_t next_addr() const { return ring0 + q * kRingStride + lane16; }
 };
-
-// The packet's last word (lane k == 0, last slot): the bytes past the packet end cleared;
-// with 16-B-aligned chunks (ENET_CRC_RAGGED_A16) the u words after it are zero as well.
-__device__ __forceinline__ void mask_last(const RaggedRound& r, uint32_t& w0, uint32_t& w1, uint32_t& w2,
-                                          uint32_t& w3) {
-#ifdef ENET_CRC_RAGGED_A16
-  const uint32_t u = (r.meta >> kMetaTShiftShift) & 3u, lm = r.last_mask;
-  w3 = u == 0 ? w3 & lm : 0u;
-  w2 = u == 1 ? w2 & lm : (u > 1 ? 0u : w2);
-  w1 = u == 2 ? w1 & lm : (u > 2 ? 0u : w1);
-  w0 = u == 3 ? w0 & lm : w0;
-#else
-  (void)w0;
-  (void)w1;
-  (void)w2;
-  w3 &= r.last_mask;
-#endif
-}
 
 // A round whose packets' top slots lie in T .. T + 1 (T .. ring - 1 in ring-length rounds)
 // and that needs no fallback: the slot loop of crc32_uniform_dma_kernel (unrolled, lookups
@@ -1644,24 +1543,14 @@ __device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const 
   for (int s = 0; s < NS; ++s) {
     const u32x4 v = R.nextv;
     const int32_t f = s + kRaggedRing;  // refill this slot's LDS slot kRaggedRing slots ahead
-#ifdef ENET_CRC_RAGGED_NT
-    // Measurement build: the slots past every top slot stream non-temporal, so the lines
-    // read at the top slots (shared with the previous packet, which reads them at its last
-    // slot about a round later) are the ones the L2 keeps.
-    if (f < NS)
-      R.dma_nt(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)f);
-    else
-      R.dma(ragged_src(nxt, f - NS, c.dummy));
-#else
     R.dma(f < NS ? cur.cb + (uint64_t)kBytesPerStep * (uint64_t)f : ragged_src(nxt, f - NS, c.dummy));
-#endif
     if (s < T) {
       R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
       issue_order_fence();
       continue;
     }
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    if (s == NS - 1) mask_last(cur, w0, w1, w2, w3);  // data only: before the injection in mask_top
+    if (s == NS - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
     // each lane's own top slot (B .. B + 1, or B .. ring - 1 in ring-length rounds)
     if (s <= (NS == kRaggedRing ? kRaggedRing - 1 : T + 1)) {
       const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
@@ -1702,21 +1591,20 @@ __device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRo
 }
 
 // Any round (mixed step counts, fallback chunks, long packets): per-lane top slot.
-template <uint32_t kStep = kBytesPerStep>
 __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
                                                      const LaneConsts& c, const uint32_t* lds, uint32_t& h0,
                                                      uint32_t& h1, uint32_t& h2, uint32_t& h3) {
   for (int32_t s = 0; s < cur.ns; ++s) {
     const u32x4 v = R.nextv;
     const int32_t f = s + kRaggedRing;
-    R.dma(f < cur.ns ? ragged_src<kStep>(cur, f, c.dummy) : ragged_src<kStep>(nxt, f - cur.ns, c.dummy));
+    R.dma(f < cur.ns ? ragged_src(cur, f, c.dummy) : ragged_src(nxt, f - cur.ns, c.dummy));
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     const bool top = s == cur.top_slot;
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
       if (top && (cur.meta & kMetaFallback))
-        load_top_words(cur.cb + (uint64_t)kStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
+        load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
     }
-    if (s == cur.ns - 1) mask_last(cur, w0, w1, w2, w3);  // data only: before the injection in mask_top
+    if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
       if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
     }
@@ -1776,9 +1664,6 @@ struct JobSlot {
 };
 struct RaggedJobsLds {
   uint32_t tables[kLdsDwords];
-#ifdef ENET_CRC_RAGGED_A16
-  uint32_t inv[1024];  // M32^-1 (back_over_padding)
-#endif
   u32x4 ring[kRaggedRing][kWavesPerBlock][64];
   JobSlot job[kJobSlots];
   uint32_t ready[kJobSlots];     // k + 1 once the workgroup's k-th job has its records here
@@ -1882,9 +1767,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     S.failed = 0;
   }
   fill_lds(lds);
-#ifdef ENET_CRC_RAGGED_A16
-  for (int x = threadIdx.x; x < 1024; x += kBlock) S.inv[x] = g_op_tables.inv1[x >> 8][x & 255];
-#endif
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1955,11 +1837,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool v = 4u * lane + i < n;
-#ifdef ENET_CRC_RAGGED_A16
-      const RaggedRecord rec = ragged_record_a16(b.base + off[i], len[i]);
-#else
       const RaggedRecord rec = ragged_record(b.base + off[i], len[i], c.base4);
-#endif
       ax[i] = v ? rec.ax | ((uint64_t)(4u * lane + i) << kJobLidShift) : 0ull;
       info[i] = rec.info;
       cls[i] = v ? (rec.nsteps < kStepClasses - 1 ? rec.nsteps : kStepClasses - 1) : (uint32_t)kStepClasses;
@@ -2087,10 +1965,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       }
     }
   };
-#ifdef ENET_CRC_PAIR_COMBINE
-  bool held = false;
-  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, pmeta = 0, pid = 0, pk = 0, pjr = 0;
-#endif
   uint32_t rnd0 = wv, rnd1 = wv + kWavesPerBlock;
   if (!round_valid(rnd0)) return;
   RaggedRound cur = make_round(rnd0);
@@ -2142,41 +2016,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     st_body += st_b1 - st_b0;
     ++st_rounds;
 #endif
-#ifdef ENET_CRC_PAIR_COMBINE
-    // Measurement build: a round whose successor is live keeps its streams (held) and is
-    // combined together with that successor, both dependent lookup chains in flight at once.
-    if (!held && nxt.live) {
-      held = true;
-      q0 = h0;
-      q1 = h1;
-      q2 = h2;
-      q3 = h3;
-      pmeta = cur.meta;
-      pid = cur.id;
-      pk = cur.job_k;
-      pjr = cur.job_rounds;
-    } else if (held) {
-      held = false;
-      uint32_t yq, y;
-      combine_tree2(lds, q0, q1, q2, q3, h0, h1, h2, h3, c.lk, yq, y);
-      const uint32_t rq = finish_word(lds, yq, (pmeta >> kMetaNTailShift) & 3u, c.lk);
-      const uint32_t rc = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);
-      publish(pk, pid, pmeta, pjr, (pmeta & kMetaEmpty) ? kInitRegister : rq);
-      publish(cur.job_k, cur.id, cur.meta, cur.job_rounds, (cur.meta & kMetaEmpty) ? kInitRegister : rc);
-    } else
-#endif
-    {
-    uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
-#ifdef ENET_CRC_RAGGED_A16
-    {  // back over the u zero words past the packet: y <- M32^-u y (lane k == 0, u = 0..3)
-      const uint32_t u = (cur.meta >> kMetaTShiftShift) & 3u;
-      if (u) {
-        y = apply_small(S.inv, y);
-        if (u > 1u) y = apply_small(S.inv, y);
-        if (u > 2u) y = apply_small(S.inv, y);
-      }
-    }
-#endif
+    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
 #ifdef ENET_CRC_ROUND_STAMPS
@@ -2184,7 +2024,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     st_comb += __builtin_amdgcn_s_memtime() - st_b1;
 #endif
     publish(cur.job_k, cur.id, cur.meta, cur.job_rounds, reg);
-    }
 #ifdef ENET_CRC_ROUND_STAMPS
     const uint64_t st_j0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2217,1318 +2056,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   __builtin_amdgcn_s_waitcnt(0);
 }
 
-
-#if defined(ENET_CRC_RAGGED16) || defined(ENET_CRC_RAGGED16W) || defined(ENET_CRC_RAGGED16D)
-// The 16-packet-round kernels below exist only in their measurement builds (DESIGN.md §4:
-// all slower than crc32_ragged_jobs_kernel); the product library does not carry their code.
-// ---------------------------------------------------------------------------------
-// Ragged kernel with rounds of 16 packets, 4 lanes per packet (ENET_CRC_RAGGED16 measurement
-// build: slower than the 8-lane kernel).  Same pipeline as crc32_ragged_jobs_kernel above (jobs sorted by step
-// class in LDS, the LDS-DMA ring, dynamic round dispatch inside the workgroup, results
-// flushed per job, the failure channel), but a group of FOUR lanes owns a packet and a
-// slot covers 64 B of it: a round carries twice the bytes for the same per-round work
-// (record decode, combine, result, flags, dispatch), which is what bound the 8-lane
-// kernel (DESIGN.md §4 "Ragged jobs kernel": instruction issue, ~250 VALU + ~300 SALU
-// of fixed work per round).
-//   * Arithmetic: chunk c (16 B, from the packet end) belongs to lane k = c % 4 at step
-//     i = c / 4; Horner operator M32^16 (the replicated block's main set); in-lane
-//     combine as before; a 2-level tree M32^4, M32^8 across the 4 lanes.
-//   * Jobs of up to 512 packets (8 per lane of the building wave) sorted by 64-B step
-//     count (classes 0..23; 24 = longer, or a chunk that may reach below the caller's
-//     buffer).  The build writes a header per round: the smallest and largest step count
-//     of its 16 packets, and whether it needs the generic body.  A round's slot count
-//     then needs no cross-lane reduction.
-//   * Round bodies: unrolled for rounds of <= 23 slots whose packets differ by <= 2 steps
-//     (after the sort, nearly all).  Every lane's top slot lies in the first three
-//     slots; there each lane masks its own top chunk (exec-masked).  Other rounds take
-//     the generic loop.
-// ---------------------------------------------------------------------------------
-constexpr int kG4 = 4;                                   // lanes per packet
-constexpr int kPW4 = 64 / kG4;                           // packets per round
-constexpr uint32_t kStep4 = 16u * kG4;                   // bytes per packet per slot
-constexpr int kLevel4 = ilog2(4 * kG4);                  // Horner operator M32^16
-constexpr int kJobPackets4 = 512;                        // 8 per lane of the building wave
-constexpr int kJobRounds4 = kJobPackets4 / kPW4;         // 32
-constexpr int kJobSlots4 = 4;                            // job slots in LDS
-constexpr int kJobAhead4 = 2;                            // jobs built ahead of the one claimed
-constexpr uint32_t kRound4Bytes = 192;                   // per round: u64 ax[16], u32 info[16]
-constexpr uint32_t kRec4Bytes = kJobRounds4 * kRound4Bytes;  // 6 KiB, also the descriptor staging
-constexpr uint32_t kClassLong4 = 24;                     // class = step count below 24; 24: the rest
-constexpr uint32_t kClassNone4 = 25;                     // no packet
-constexpr int kFast4Max = (int)kClassLong4 - 1;          // unrolled bodies up to 23 slots (1472 B)
-constexpr uint32_t kHeadGeneric = 1u << 16;              // round header bit: generic body
-constexpr int kJobLidShift4 = 54;                        // local id (0..511) in ax bits 54..62
-static_assert(kRec4Bytes == kJobPackets4 * 12, "staging: u64 offsets + u32 lengths");
-static_assert((kJobSlots4 & (kJobSlots4 - 1)) == 0, "slot = job & (slots - 1)");
-constexpr int kRing16 = 3;  // ring slots per wave (Ring3; top slots 0..2 are issued by the previous round)
-
-struct JobSlot4 {
-  u32x4 rec[kRec4Bytes / 16];
-  uint32_t head[kJobRounds4];  // per round: min steps | max steps << 8 | kHeadGeneric
-  uint32_t hist[32];           // job build: packets per class, then each class's first position
-  uint32_t res[kJobPackets4];
-};
-struct Ragged16Lds {
-  uint32_t tables[kRepDwords + 2 * 1024];  // replicated M32^16 | M32^1 block, then M32^4 and M32^8
-  u32x4 ring[kRing16][kWavesPerBlock][64];
-  JobSlot4 job[kJobSlots4];
-  uint32_t ready[kJobSlots4];     // k + 1 once the workgroup's k-th job has its records here
-  uint32_t consumed[kJobSlots4];  // rounds of the slot's job whose records have been read
-  uint32_t done[kJobSlots4];      // rounds of the job whose checksums are in res
-  uint32_t freed[kJobSlots4];     // k + 1 once the k-th job's checksums are in HBM
-  uint32_t next_dispatch;
-  uint32_t failed;                // != 0 once a wave gave up a wait (report_fault)
-};
-static_assert(sizeof(Ragged16Lds) <= 160 * 1024, "LDS");
-
-__device__ __forceinline__ void fill_lds4(uint32_t* lds) {
-  fill_replicated(lds, kLevel4);
-  for (int x = threadIdx.x; x < 2 * 1024; x += kBlock) {
-    const int set = x >> 10, rem = x & 1023;  // set l: M32^(4 * 2^l)
-    lds[kRepDwords + x] = g_op_tables.op[set + 2][rem >> 8][rem & 255];
-  }
-}
-
-// ragged_record for 64-B steps: nsteps = ceil(nwords / 16), pad = 64 nsteps - 4 nwords
-// (0..60); same ax / info fields.
-__device__ __forceinline__ RaggedRecord ragged_record4(uint64_t sa, uint32_t len, uint64_t base4) {
-  const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
-  const uint64_t a1 = sa + len + z, top = sa & ~(uint64_t)3;
-  const uint32_t nwords = (uint32_t)((a1 - top) >> 2);
-  const uint32_t nsteps = (nwords + 15u) >> 4;
-  const uint32_t pad = kStep4 * nsteps - 4u * nwords;
-  const uint64_t near = top - base4 < 16 ? 1ull : 0ull;
-  RaggedRecord r;
-  r.ax = a1 | ((sa & 3u) << kRecVShift) | ((uint64_t)z << kRecZShift) | (near << kRecNearBit) | (1ull << kRecValidBit);
-  r.info = nsteps | ((pad >> 2) << kRecPadShift);
-  r.nsteps = nsteps;
-  return r;
-}
-
-// Per-lane round state from the group's record and the round header (hdr, wave-uniform).
-__device__ __forceinline__ RaggedRound round16_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t hdr,
-                                                           const LaneConsts& c) {
-  const uint32_t k = threadIdx.x & (kG4 - 1);
-  const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
-  const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
-  const uint32_t pad = (info >> kRecPadShift) << 2;
-  const uint32_t v = valid ? (uint32_t)(ax >> kRecVShift) & 3u : 0u;
-  const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
-  const int32_t nsmin = (int32_t)(hdr & 255u), nsmax = (int32_t)((hdr >> 8) & 255u);
-  const bool generic = (hdr & kHeadGeneric) != 0u || nsmax == 0;
-  int32_t mx = nsmax;
-  if (generic) {  // rare: the header does not bound the round
-    mx = __builtin_amdgcn_readlane(nsteps, 0);
-#pragma unroll
-    for (int g = 1; g < kPW4; ++g) mx = max(mx, __builtin_amdgcn_readlane(nsteps, g * kG4));
-  }
-  RaggedRound rr;
-  rr.ns = max(kRing16, mx);
-  rr.cb = a1 - 16u * (uint64_t)(k + 1u) - (uint64_t)kStep4 * (uint64_t)(rr.ns - 1);
-  rr.top_slot = rr.ns - nsteps;
-  // This lane's chunk at the top step, relative to top: 4 nwords - 16 (k + 4 (nsteps - 1) + 1)
-  // = 48 - 16 k - pad.
-  const int32_t rel = 48 - 16 * (int32_t)k - (int32_t)pad;
-  const bool inside = nsteps > 0 && rel > -16;
-  bool fb = false;
-  if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
-    const uint64_t top = a1 - ((uint64_t)kStep4 * (uint64_t)nsteps - pad);
-    fb = top - c.base4 < (uint64_t)(-rel);
-  }
-  const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
-  rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
-            (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
-  rr.last_mask = k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
-  rr.id = (uint32_t)(ax >> kJobLidShift4) & (uint32_t)(kJobPackets4 - 1);
-  rr.top_uniform = rr.ns - nsmax;  // B: the first top slot of a fast round
-  rr.spread = nsmax - nsmin;
-  rr.fast = !generic && rr.ns <= kFast4Max && (rr.ns == kRing16 || rr.spread <= 2);
-  return rr;
-}
-
-// The LDS-DMA ring of crc32_ragged16_kernel (3 KiB per wave, 1 KiB per position), with its
-// positions in consumption order: slot s of the current round lands in position a[s % 3].
-// Unrolled bodies index it with their compile-time slot number, so a slot costs no ring
-// arithmetic (one M0 write); at a round's end the order rotates by the round's slot count.
-struct Ring3 {
-  uint32_t a0, a1, a2;  // wave-uniform LDS byte addresses
-  uint32_t lane16;      // lane * 16
-  u32x4 nextv;          // landed data of the slot about to be consumed
-  template <int S>
-  __device__ __forceinline__ uint32_t at() const {
-    return S % 3 == 0 ? a0 : (S % 3 == 1 ? a1 : a2);
-  }
-  __device__ __forceinline__ uint32_t at_rt(uint32_t m) const { return m == 0 ? a0 : (m == 1 ? a1 : a2); }
-  __device__ __forceinline__ void rotate(uint32_t r) {  // r = slots consumed, mod 3
-    const uint32_t b0 = a0, b1 = a1, b2 = a2;
-    a0 = r == 0 ? b0 : (r == 1 ? b1 : b2);
-    a1 = r == 0 ? b1 : (r == 1 ? b2 : b0);
-    a2 = r == 0 ? b2 : (r == 1 ? b0 : b1);
-  }
-};
-
-// One 16-B LDS-DMA per lane from `src` into the ring position at LDS byte address `lds`.
-// (No immediate offset: the instruction applies it to the LDS address as well as to the
-// global one, so a step offset there would land the data past the ring position.)
-__device__ __forceinline__ void dma16(uint64_t src, uint32_t lds) {
-  __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)(uintptr_t)lds, 16, 0, 0);
-}
-
-// Per-lane masks of a lane's top chunk from round_meta(): w_j <- (w_j & am_j) ^ xm_j keeps
-// the packet's own bytes and injects the initial register (mask_top); the identity for lanes
-// whose top chunk lies wholly inside the packet.
-struct TopMasks {
-  uint32_t am0, am1, am2, am3, xm0, xm1, xm2, xm3;
-};
-__device__ __forceinline__ TopMasks top_masks(uint32_t meta) {
-  const uint32_t head = meta & kMetaHeadMask;
-  const uint32_t v = (meta >> kMetaVShift) & 3u;
-  const uint32_t keep = 0xFFFFFFFFu << (8u * v), kk = head_k(v);
-  const int32_t j0 = head ? 4 - (int32_t)head : -1;  // word index of the top word (-1: no mask)
-  TopMasks m;
-  m.am0 = j0 > 0 ? 0u : (j0 == 0 ? keep : 0xFFFFFFFFu);
-  m.am1 = j0 > 1 ? 0u : (j0 == 1 ? keep : 0xFFFFFFFFu);
-  m.am2 = j0 > 2 ? 0u : (j0 == 2 ? keep : 0xFFFFFFFFu);
-  m.am3 = j0 == 3 ? keep : 0xFFFFFFFFu;
-  m.xm0 = j0 == 0 ? kk : 0u;
-  m.xm1 = j0 == 1 ? kk : 0u;
-  m.xm2 = j0 == 2 ? kk : 0u;
-  m.xm3 = j0 == 3 ? kk : 0u;
-  return m;
-}
-__device__ __forceinline__ uint32_t and_xor(uint32_t w, uint32_t a, uint32_t x) {
-  return (w & a) ^ x;  // one v_bitop3
-}
-
-// A fast round: NS unrolled slots.  Lane tops lie in slots B..B + spread (all < the ring,
-// so the previous round issued their DMAs with per-lane sources: the zero chunk before a
-// lane's top); each lane masks its own top chunk there.  Slot B starts the streams without
-// lookups (a stream is zero before its lane's top).  Slots before B (NS == ring) are only
-// consumed.
-template <int S, int NS, int B>
-__device__ __forceinline__ void round16_slot(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
-                                             const LaneConsts& c, const TopMasks& m, uint32_t& h0, uint32_t& h1,
-                                             uint32_t& h2, uint32_t& h3) {
-  constexpr int kF = S + kRing16;  // refill this slot's position kRing16 slots ahead
-  const u32x4 v = R.nextv;
-  if constexpr (kF < NS)
-    dma16(cur.cb + (uint64_t)kStep4 * kF, R.at<S>());  // inside every valid packet (kF > its top slot)
-  else
-    dma16(ragged_src<kStep4>(nxt, kF - NS, c.dummy), R.at<S>());
-  const uint32_t next_addr = R.at<S + 1>() + R.lane16;
-  if constexpr (S < B) {
-    R.nextv = read_landed_slot<kRing16 - 1>(next_addr);
-  } else {
-    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    if constexpr (S == NS - 1) w3 &= cur.last_mask;  // data only: before the injection
-    if constexpr (S < kRing16) {
-      if (NS == kRing16 || S - B <= cur.spread) {
-        if (cur.top_slot == S) {
-          w0 = and_xor(w0, m.am0, m.xm0);
-          w1 = and_xor(w1, m.am1, m.xm1);
-          w2 = and_xor(w2, m.am2, m.xm2);
-          w3 = and_xor(w3, m.am3, m.xm3);
-        }
-      }
-    }
-    if constexpr (S == B) {
-      h0 = w0;  // M32^16(0) = 0: no lookups
-      h1 = w1;
-      h2 = w2;
-      h3 = w3;
-      R.nextv = read_landed_slot<kRing16 - 1>(next_addr);
-    } else {
-      horner_step_and_read<kRing16 - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
-    }
-  }
-  issue_order_fence();
-}
-
-template <int NS, int B, int... S>
-__device__ __forceinline__ void round16_slots(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
-                                              const LaneConsts& c, const TopMasks& m, uint32_t& h0, uint32_t& h1,
-                                              uint32_t& h2, uint32_t& h3, std::integer_sequence<int, S...>) {
-  (round16_slot<S, NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3), ...);
-}
-
-template <int NS, int B>
-__device__ __forceinline__ void round16_fast(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
-                                             const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                             uint32_t& h3) {
-  static_assert(B == 0 || NS == kRing16, "leading consumed slots only in ring-length rounds");
-  const TopMasks m = top_masks(cur.meta);
-  round16_slots<NS, B>(cur, nxt, R, c, m, h0, h1, h2, h3, std::make_integer_sequence<int, NS>{});
-  R.rotate((uint32_t)(NS % 3));
-}
-
-// Any round (wider spreads, longer packets, chunks below the caller's buffer): per-lane top
-// slot, runtime slot count.
-__device__ __forceinline__ void round16_generic(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
-                                                const LaneConsts& c, const uint32_t* lds, uint32_t& h0,
-                                                uint32_t& h1, uint32_t& h2, uint32_t& h3) {
-  uint32_t m = 0;  // s % 3
-  for (int32_t s = 0; s < cur.ns; ++s) {
-    const u32x4 v = R.nextv;
-    const int32_t f = s + kRing16;
-    const uint64_t src = f < cur.ns ? ragged_src<kStep4>(cur, f, c.dummy) : ragged_src<kStep4>(nxt, f - cur.ns, c.dummy);
-    dma16(src, R.at_rt(m));
-    m = m == 2u ? 0u : m + 1u;
-    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    const bool top = s == cur.top_slot;
-    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
-      if (top && (cur.meta & kMetaFallback))
-        load_top_words(cur.cb + (uint64_t)kStep4 * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
-    }
-    if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
-    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
-      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
-    }
-    h0 = horner_main(lds, h0, w0, c.lk);
-    h1 = horner_main(lds, h1, w1, c.lk);
-    h2 = horner_main(lds, h2, w2, c.lk);
-    h3 = horner_main(lds, h3, w3, c.lk);
-    R.nextv = read_landed_slot<kRing16 - 1>(R.at_rt(m) + R.lane16);
-    issue_order_fence();
-  }
-  R.rotate(m);
-}
-
-template <int... I>
-__device__ __forceinline__ bool round16_dispatch(const RaggedRound& cur, const RaggedRound& nxt, Ring3& R,
-                                                 const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                                 uint32_t& h3, std::integer_sequence<int, I...>) {
-  if (cur.ns == kRing16) {
-    if (cur.top_uniform == 0) round16_fast<kRing16, 0>(cur, nxt, R, c, h0, h1, h2, h3);
-    else if (cur.top_uniform == 1) round16_fast<kRing16, 1>(cur, nxt, R, c, h0, h1, h2, h3);
-    else if (cur.top_uniform == 2) round16_fast<kRing16, 2>(cur, nxt, R, c, h0, h1, h2, h3);
-    else return false;
-    return true;
-  }
-  return ((cur.ns == I + kRing16 + 1 ? (round16_fast<I + kRing16 + 1, 0>(cur, nxt, R, c, h0, h1, h2, h3), true)
-                                         : false) ||
-          ...);
-}
-
-// The 4 word streams of each of the group's 4 lanes combined into y (register = M32 y),
-// valid on lane k == 0: in-lane Horner with M32^1 (replicated, conflict-free), then the
-// 2-level tree M32^4, M32^8 (unreplicated; only the lanes whose value moves look up).
-__device__ __forceinline__ uint32_t combine_tree4(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
-                                                  uint32_t h3, const Lookup& lk) {
-  uint32_t y = apply_rep(lds, h0, h1, lk.lp1, lk);
-  y = apply_rep(lds, y, h2, lk.lp1, lk);
-  y = apply_rep(lds, y, h3, lk.lp1, lk);
-  const uint32_t k = threadIdx.x & (kG4 - 1);
-  uint32_t t = 0;
-  if (k & 1u) t = apply_small(lds + kRepDwords, y);
-  y ^= from_lane_plus<1>(t);
-  if (k == 2u) t = apply_small(lds + kRepDwords + 1024, y);
-  y ^= from_lane_plus<2>(t);
-  return y;
-}
-
-__device__ __forceinline__ void lds_st8_nowait(uint32_t a, uint32_t v) {
-  asm volatile("ds_write_b8 %0, %1" : : "v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
-  asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
-}
-
-__global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
-  send_servers_home();
-  constexpr int kDmaRing = kRing16;
-  __shared__ __attribute__((aligned(16))) Ragged16Lds S;
-  uint32_t* const lds = S.tables;
-  constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
-  if (threadIdx.x < (unsigned)kJobSlots4) {
-    S.ready[threadIdx.x] = 0;
-    S.consumed[threadIdx.x] = 0;
-    S.done[threadIdx.x] = 0;
-    S.freed[threadIdx.x] = 0;
-  }
-  if (threadIdx.x == 0) {
-    S.next_dispatch = kWavesPerBlock * kLook;
-    S.failed = 0;
-  }
-  fill_lds4(lds);
-  __syncthreads();
-  const LaneConsts c = lane_consts(b.base);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t k4 = lane & (kG4 - 1), g4 = lane / kG4;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
-
-  auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
-  const uint32_t JP = b.job_packets;
-  auto job_count = [&](uint64_t J) -> uint32_t {  // packets in job J (J < njobs)
-    const uint64_t left = b.count - J * JP;
-    return left < (uint64_t)JP ? (uint32_t)left : JP;
-  };
-  // Round d of this workgroup: round d % RJ of its (d / RJ)-th job (d / RJ as one s_mul_hi,
-  // exact below 2^27 rounds: launch_ragged checks).
-  const uint32_t RJ = JP / kPW4;
-  const uint32_t rj_magic = 0xFFFFFFFFu / RJ + 1u;
-  auto div_rj = [&](uint32_t x) -> uint32_t { return __umulhi(x, rj_magic); };
-  auto round_valid = [&](uint32_t d) -> bool {
-    const uint32_t k = div_rj(d);
-    const uint64_t J = job_of(k);
-    return J < b.njobs && (uint64_t)(d - k * RJ) * kPW4 < job_count(J);
-  };
-
-  // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
-  // u32 lengths at +4096): six 16-B DMAs per lane, or, near the batch end, 24 4-B DMAs
-  // clamped to the batch.
-  auto job_dma = [&](uint64_t J, uint32_t slot) {
-    LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
-    const uint64_t p0 = J * JP;
-    if (p0 + kJobPackets4 <= b.count) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 * i + 2 * lane), (LdsVoid*)(st + 1024 * i),
-                                         16, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 256 * i + 4 * lane),
-                                         (LdsVoid*)(st + 4096 + 1024 * i), 16, 0, 0);
-    } else {
-      // Not unrolled: one address live at a time (see crc32_ragged_jobs_kernel).
-      const uint32_t* offw = reinterpret_cast<const uint32_t*>(b.offsets);
-#pragma unroll 1
-      for (uint32_t i = 0; i < 24; ++i) {
-        const uint32_t w = 64u * (i & 15u) + lane;
-        const uint64_t e = i < 16 ? p0 + w / 2 : p0 + 64u * (i - 16u) + lane;
-        const void* src = e >= b.count ? (const void*)g_zero_chunk
-                          : i < 16   ? (const void*)(offw + 2 * e + (w & 1u))
-                                     : (const void*)(b.lengths + e);
-        __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 256 * i), 4, 0, 0);
-      }
-    }
-  };
-  // Phase B (>= kDmaRing DMAs after phase A): sort the job's packets by step class, write
-  // its round records and headers in place of the descriptors, then mark the slot ready.
-  // The sort is a histogram in LDS: each packet's ds_add_rtn on its class counter returns
-  // its rank in the class (in some lane order; results go out by local id, so any order
-  // is right), one wave scan turns the counts into first positions.
-  auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
-    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDmaRing - 1) : "memory");
-    const uint32_t st = lds_addr(&S.job[slot].rec[0]);
-    const uint32_t hd = lds_addr(&S.job[slot].head[0]);
-    const uint32_t hi = lds_addr(&S.job[slot].hist[0]);
-    const uint32_t n = job_count(J);
-    // Lane id from an asm statement: the compiler cannot hoist the per-packet local ids
-    // out of the round loop (hoisted, they were spilled to scratch).
-    uint32_t ln8;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 3, %0"
-                 : "=v"(ln8));
-    if (lane < 32u) {
-      lds_st32_nowait(hi + 4u * lane, 0u);
-      lds_st32_nowait(hd + 4u * lane, 0u);
-    }
-    uint64_t ax[8];
-    uint32_t info[8], cls[8], pos[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // 4 packets at a time: 8B offsets at 8 id, lengths at 4096 + 4 id
-      const u32x4 o01 = lds_ld128(st + 8u * ln8 + 32u * h), o23 = lds_ld128(st + 8u * ln8 + 32u * h + 16u);
-      const u32x4 ll = lds_ld128(st + 4096u + 4u * ln8 + 16u * h);
-      const uint64_t off[4] = {o01.x | (uint64_t)o01.y << 32, o01.z | (uint64_t)o01.w << 32,
-                               o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
-      const uint32_t len[4] = {ll.x, ll.y, ll.z, ll.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = 4 * h + j;
-        const uint32_t id = ln8 + (uint32_t)i;
-        const bool v = id < n;
-        const RaggedRecord rec = ragged_record4(b.base + off[j], len[j], c.base4);
-        ax[i] = v ? rec.ax | ((uint64_t)id << kJobLidShift4) : 0ull;
-        info[i] = rec.info;
-        // Longer packets and chunks that may reach below the caller's buffer sort last,
-        // in the class whose rounds take the generic body.
-        const bool lng = rec.nsteps >= kClassLong4 || ((rec.ax >> kRecNearBit) & 1u);
-        cls[i] = !v ? kClassNone4 : (lng ? kClassLong4 : rec.nsteps);
-      }
-    }
-    // Ranks in the class (the adds follow the zeroing above: one wave, LDS in order).
-#pragma unroll
-    for (int i = 0; i < 8; ++i) pos[i] = lds_add_rtn(hi + 4u * cls[i], 1u);
-    uint32_t cnt = 0;  // counts -> first positions (exclusive scan over the classes, whole wave)
-    if (lane < 32u) cnt = lds_ld32(hi + 4u * lane);
-    const uint32_t first = wave_inclusive_add(cnt) - cnt;
-    if (lane < 32u) lds_st32(hi + 4u * lane, first);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t q = lds_ld32(hi + 4u * cls[i]) + pos[i];
-      const uint32_t r = st + (q >> 4) * kRound4Bytes;
-      lds_st64(r + 8u * (q & 15u), ax[i]);
-      lds_st32(r + 128u + 4u * (q & 15u), info[i]);
-      if (cls[i] != kClassNone4) {
-        const uint32_t h = hd + 4u * (q >> 4);
-        const uint32_t ns8 = min(info[i] & kRecStepsMask, 255u);
-        if ((q & 15u) == 0u) lds_st8_nowait(h, ns8);
-        if ((q & 15u) == 15u || q + 1u == n) lds_st8_nowait(h + 1u, ns8);
-        // Longer packets, chunks near the caller's base, and the job's partial last round:
-        // its empty groups' chunk addresses lie below the base, which only the generic
-        // body's per-lane sources keep from being read.
-        if (cls[i] == kClassLong4 || ((q & 15u) != 15u && q + 1u == n)) lds_or_nowait(h, kHeadGeneric);
-      }
-    }
-    if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);  // waits for every LDS write above
-  };
-
-  // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
-  // (rounds 0 .. 2 x 16 - 1) and kJobAhead4 more.  RJ >= 16 (launch_ragged), so that is at
-  // most 2 + kJobAhead4 = kJobSlots4 jobs.
-  const uint32_t first_jobs = (kWavesPerBlock * kLook - 1) / RJ + kJobAhead4 + 1;
-  if (wv < first_jobs && job_of(wv) < b.njobs) {
-    job_dma(job_of(wv), wv);
-    __builtin_amdgcn_s_waitcnt(0);
-    job_build(job_of(wv), wv, wv + 1u);
-  }
-  __syncthreads();
-
-  uint32_t seen_ready = 0, seen_freed = 0;
-  const uint32_t fail_a = lds_addr(&S.failed);
-  auto waited = [&](uint32_t w, uint32_t bit) -> bool {
-    if (w == kWaitGaveUp) report_fault(fail_a, bit);
-    return w == kWaitOk;
-  };
-  auto make_round = [&](uint32_t d) -> RaggedRound {
-    uint64_t ax = 0;
-    uint32_t info = 0, hdr = 0;
-    const uint32_t k = div_rj(d), slot = k & (uint32_t)(kJobSlots4 - 1), rj = d - k * RJ;
-    const uint64_t J = job_of(k);
-    const uint32_t n = J < b.njobs ? job_count(J) : 0u;
-    const bool live = rj * kPW4 < n;  // round_valid(d)
-    bool rv = live;
-    if (rv && k + 1u > seen_ready) {
-      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
-      if (rv) seen_ready = k + 1u;
-    }
-#ifdef ENET_CRC_TEST_HOOKS
-    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k) rv = waited(kWaitGaveUp, kFaultReady);
-#endif
-    if (rv) {
-      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + rj * kRound4Bytes;
-      asm volatile("ds_read_b64 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(ax), "=&v"(info), "=&v"(hdr)
-                   : "v"(r + 8u * g4), "v"(r + 128u + 4u * g4), "v"(lds_addr(&S.job[slot].head[rj]))
-                   : "memory");
-      hdr = __builtin_amdgcn_readfirstlane(hdr);
-      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
-    }
-    RaggedRound rr = round16_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), hdr, c);
-    rr.live = live;
-    rr.job_k = k;
-    rr.job_rounds = (n + kPW4 - 1) / kPW4;
-    return rr;
-  };
-
-  uint32_t rnd0 = wv, rnd1 = wv + kWavesPerBlock;
-  if (!round_valid(rnd0)) return;
-  RaggedRound cur = make_round(rnd0);
-  RaggedRound nxt = make_round(rnd1);
-  Ring3 R;
-  R.a0 = lds_addr(&S.ring[0][wv][0]);
-  R.a1 = lds_addr(&S.ring[1][wv][0]);
-  R.a2 = lds_addr(&S.ring[2][wv][0]);
-  R.lane16 = lane * 16u;
-  dma16(ragged_src<kStep4>(cur, 0, c.dummy), R.a0);  // cur.ns >= kDmaRing
-  dma16(ragged_src<kStep4>(cur, 1, c.dummy), R.a1);
-  dma16(ragged_src<kStep4>(cur, 2, c.dummy), R.a2);
-  R.nextv = read_landed_slot<kDmaRing - 1>(R.a0 + R.lane16);
-  while (cur.live) {  // cur is round rnd0
-    uint32_t d = 0;
-    if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
-    d = __builtin_amdgcn_readfirstlane(d);
-    // Build duty: the claimer of a job's first round builds the job kJobAhead4 later once
-    // every round of the slot's previous job has read its record (crc32_ragged_jobs_kernel).
-    bool build = false;
-    const uint32_t kd = div_rj(d), kb = kd + kJobAhead4, bslot = kb & (uint32_t)(kJobSlots4 - 1);
-    if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
-      build = kb < (uint32_t)kJobSlots4 ||
-              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
-      if (build) {
-        if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
-        job_dma(job_of(kb), bslot);
-      }
-    }
-    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    if (!cur.fast || !round16_dispatch(cur, nxt, R, c, h0, h1, h2, h3,
-                                       std::make_integer_sequence<int, kFast4Max - kRing16>{}))
-      round16_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
-    const uint32_t y = combine_tree4(lds, h0, h1, h2, h3, c.lk);
-    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k4 == 0 holds it
-    if (cur.meta & kMetaEmpty) reg = kInitRegister;
-    // The round's checksums into the job's result array; the last round of a job writes
-    // the job's checksums to HBM.
-    const uint32_t k0 = cur.job_k, slot0 = k0 & (uint32_t)(kJobSlots4 - 1);
-    if (k0 >= (uint32_t)kJobSlots4 && k0 + 1u - (uint32_t)kJobSlots4 > seen_freed) {
-      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots4 + 1u, fail_a), kFaultFreed))
-        seen_freed = k0 + 1u - (uint32_t)kJobSlots4;
-    }
-    if (k4 == 0 && (cur.meta & kMetaStore))
-      lds_st32_nowait(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
-    uint32_t old = 0;
-    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old + 1u == cur.job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
-      const uint64_t J0 = job_of(k0);
-      const uint32_t n0 = job_count(J0);
-      const uint32_t ra = lds_addr(&S.job[slot0].res[0]) + 32u * lane;
-      u32x4 v0, v1;
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(v0), "=&v"(v1)
-                   : "v"(ra), "v"(ra + 16u)
-                   : "memory");
-      uint32_t* dst = out + J0 * JP + 8u * lane;
-      if (8u * lane + 8u <= n0) {
-        reinterpret_cast<U32x4A4*>(dst)->v = v0;
-        reinterpret_cast<U32x4A4*>(dst + 4)->v = v1;
-      } else {
-        const uint32_t e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-        for (int i = 0; i < 7; ++i)
-          if (8u * lane + (uint32_t)i < n0) dst[i] = e[i];
-      }
-    }
-    if (old + 1u == cur.job_rounds && lane == 0) {
-      lds_st32(lds_addr(&S.done[slot0]), 0u);
-      lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
-    }
-    if (build) job_build(job_of(kb), bslot, kb + 1u);
-    const RaggedRound after = make_round(d);
-    rnd0 = rnd1;
-    rnd1 = d;
-    cur = nxt;
-    nxt = after;
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-}
-
-// ---------------------------------------------------------------------------------
-// Ragged kernel with 16-packet rounds loaded as 128-B pieces (crc32_ragged16w_kernel).
-// The 16-packet kernel above halves the per-round work per byte, but its DMAs move 64-B
-// pieces of 16 packets and stream slower than the 8-lane kernel's 128-B pieces of 8
-// (DESIGN.md §4).  Here the two are split: a slot is loaded the 8-lane way -- two LDS-DMA
-// instructions, instruction i's lane 8j + k reading chunk k of packet 8i + j's 128-B piece
-// -- and computed the 4-lane way: lane 4p + k reads chunks k + 4 and k of packet p's piece
-// from LDS and runs two Horner steps (M32^16) per slot, streams and combine exactly as in
-// the 16-packet kernel.  A slot is 2 KiB per wave, the ring 2 slots deep (64 KiB per CU in
-// flight); jobs of 256 packets (16 rounds) sorted by 128-B step count with round headers;
-// unrolled bodies for rounds of <= 13 slots whose step counts differ by <= 1.
-// ---------------------------------------------------------------------------------
-constexpr int kRingW = 2;                                  // ring slots per wave (2 KiB each)
-constexpr int kJobPacketsW = 256;                          // 4 per lane of the building wave
-constexpr int kJobRoundsW = kJobPacketsW / kPW4;           // 16
-constexpr int kJobSlotsW = 4;                              // job slots in LDS
-constexpr int kJobAheadW = 2;                              // jobs built ahead of the one claimed
-constexpr uint32_t kRoundWBytes = 192;                     // per round: u64 ax[16], u32 info[16]
-constexpr uint32_t kRecWBytes = kJobRoundsW * kRoundWBytes;  // 3 KiB, also the descriptor staging
-constexpr uint32_t kClassLongW = 14;                       // class = 128-B step count below 14; 14: the rest
-constexpr uint32_t kClassNoneW = 15;                       // no packet
-constexpr int kFastWMax = (int)kClassLongW - 1;            // unrolled bodies up to 13 slots (1664 B)
-constexpr uint32_t kInstrStrideW = kWavesPerBlock * 1024;  // LDS bytes between a slot's two DMA areas
-constexpr uint32_t kMetaTopHi = 1u << 13;                  // the top word lies in chunk k + 4 (else chunk k)
-static_assert(kRecWBytes == kJobPacketsW * 12, "staging: u64 offsets + u32 lengths");
-static_assert(kJobRoundsW == 16, "round d of a workgroup: job d >> 4, round d & 15");
-
-struct JobSlotW {
-  u32x4 rec[kRecWBytes / 16];
-  uint32_t head[kJobRoundsW];  // per round: min steps | max steps << 8 | kHeadGeneric
-  uint32_t hist[16];           // job build: packets per class, then each class's first position
-  uint32_t res[kJobPacketsW];
-};
-template <bool kDual>
-struct RaggedWLds {
-  // kDual: replicated M32^32 | M32^1 block, then M32^4, M32^8, M32^16 (fill_lds); else the
-  // replicated M32^16 | M32^1 block, then M32^4 and M32^8 (fill_lds4).
-  uint32_t tables[kDual ? kLdsDwords : kRepDwords + 2 * 1024];
-  u32x4 ring[kRingW][2][kWavesPerBlock][64];
-  JobSlotW job[kJobSlotsW];
-  uint32_t ready[kJobSlotsW];     // k + 1 once the workgroup's k-th job has its records here
-  uint32_t consumed[kJobSlotsW];  // rounds of the slot's job whose records have been read
-  uint32_t done[kJobSlotsW];      // rounds of the job whose checksums are in res
-  uint32_t freed[kJobSlotsW];     // k + 1 once the k-th job's checksums are in HBM
-  uint32_t next_dispatch;
-  uint32_t failed;                // != 0 once a wave gave up a wait (report_fault)
-};
-static_assert(sizeof(RaggedWLds<false>) <= 160 * 1024 && sizeof(RaggedWLds<true>) <= 160 * 1024, "LDS");
-
-// A lane's plan for one round: the sources of its two DMAs per slot (packets lane / 8 and
-// 8 + lane / 8, chunk lane % 8) and the state of its two Horner chunks (packet lane / 4,
-// chunks lane % 4 + 4 and lane % 4).
-struct RoundW {
-  uint64_t cb0, cb1;  // DMA: this lane's chunk address at slot 0, instruction 0 / 1 packet
-  int32_t top0, top1; // DMA: those packets' top slots (ns: no packet data)
-  uint32_t direct;    // DMA: bit i: instruction i's top chunk is read (inside, no fallback)
-  uint64_t cbc;       // compute: chunk k's address at slot 0 (chunk k + 4 lies 64 B below)
-  int32_t top_slot;   // compute: the packet's top slot
-  uint32_t meta;      // compute: head (of the chunk holding the top word), v, empty, z, store, fallback, kMetaTopHi
-  uint32_t last_mask; // compute: lane k == 0 clears the bytes past the packet end in the last word
-  uint32_t id;        // local id of the lane's packet in its job
-  int32_t ns;         // slots of the round (wave-uniform)
-  int32_t B;          // first top slot of a fast round
-  int32_t spread;     // max - min step count of the round's packets
-  bool fast, live;
-  uint32_t job_k, job_rounds;
-};
-
-// Source of instruction i's slot-s DMA (the zero chunk before the packet's top).
-[[maybe_unused]] __device__ __forceinline__ uint64_t srcw(const RoundW& r, int i, int32_t s, uint64_t dummy) {
-  const uint64_t cb = i ? r.cb1 : r.cb0;
-  const int32_t top = i ? r.top1 : r.top0;
-  const bool real = s > top || (s == top && ((r.direct >> i) & 1u));
-  return real ? cb + (uint64_t)kBytesPerStep * (uint64_t)s : dummy;
-}
-
-// DMA plan of one of the lane's two DMA packets (ragged_record fields, 128-B steps).
-__device__ __forceinline__ void dma_plan_w(uint64_t ax, uint32_t info, bool valid, int32_t ns, uint32_t k8,
-                                           const LaneConsts& c, uint64_t& cb, int32_t& top, bool& direct) {
-  const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
-  const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
-  const uint32_t pad = (info >> kRecPadShift) << 2;
-  cb = a1 - 16u * (uint64_t)(k8 + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(ns - 1);
-  top = ns - nsteps;
-  const int32_t rel = 112 - 16 * (int32_t)k8 - (int32_t)pad;  // chunk k8 at the top step, from the packet top
-  const bool inside = nsteps > 0 && rel > -16;
-  bool fb = false;
-  if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
-    const uint64_t t = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
-    fb = t - c.base4 < (uint64_t)(-rel);
-  }
-  direct = inside && !fb;
-}
-
-// A lane's round plan from the three records it reads and the round header.
-[[maybe_unused]] __device__ __forceinline__ RoundW roundw_from_records(uint64_t axc, uint32_t ic, uint64_t ax0, uint32_t i0,
-                                                      uint64_t ax1, uint32_t i1, bool rv, uint32_t hdr,
-                                                      const LaneConsts& c) {
-  const uint32_t lane = threadIdx.x & 63u, kc = lane & 3u, k8 = lane & 7u;
-  const bool vc = rv && ((axc >> kRecValidBit) & 1u);
-  const int32_t nsc = vc ? (int32_t)(ic & kRecStepsMask) : 0;
-  const int32_t nsmin = (int32_t)(hdr & 255u), nsmax = (int32_t)((hdr >> 8) & 255u);
-  const bool generic = (hdr & kHeadGeneric) != 0u || nsmax == 0;
-  int32_t mx = nsmax;
-  if (generic) {  // rare: the header does not bound the round
-    mx = __builtin_amdgcn_readlane(nsc, 0);
-#pragma unroll
-    for (int g = 1; g < kPW4; ++g) mx = max(mx, __builtin_amdgcn_readlane(nsc, g * kG4));
-  }
-  RoundW r;
-  r.ns = max(kRingW, mx);
-  bool d0, d1;
-  dma_plan_w(ax0, i0, rv && ((ax0 >> kRecValidBit) & 1u), r.ns, k8, c, r.cb0, r.top0, d0);
-  dma_plan_w(ax1, i1, rv && ((ax1 >> kRecValidBit) & 1u), r.ns, k8, c, r.cb1, r.top1, d1);
-  r.direct = (d0 ? 1u : 0u) | (d1 ? 2u : 0u);
-  // Compute side: chunks kc + 4 (rel1) and kc (rel1 + 64) at the top step, from the top.
-  const uint64_t a1 = vc ? (axc & kRecAddrMask) : c.base4;
-  const uint32_t pad = (ic >> kRecPadShift) << 2;
-  const uint32_t v = vc ? (uint32_t)(axc >> kRecVShift) & 3u : 0u;
-  const uint32_t z = vc ? (uint32_t)(axc >> kRecZShift) & 3u : 0u;
-  r.cbc = a1 - 16u * (uint64_t)(kc + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(r.ns - 1);
-  r.top_slot = r.ns - nsc;
-  const int32_t rel1 = 48 - 16 * (int32_t)kc - (int32_t)pad, rel0 = rel1 + 64;
-  const bool hi = nsc > 0 && rel1 > -16 && rel1 <= 0;  // the top word is in chunk kc + 4
-  const bool lo = nsc > 0 && rel0 > -16 && rel0 <= 0;  // ... in chunk kc
-  const int32_t rel = hi ? rel1 : rel0;
-  bool fb = false;
-  if (((axc >> kRecNearBit) & 1u) && vc && (hi || lo) && rel < 0) {
-    const uint64_t t = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsc - pad);
-    fb = t - c.base4 < (uint64_t)(-rel);
-  }
-  const uint32_t head = hi || lo ? (uint32_t)(rel / 4 + 4) : 0u;
-  r.meta = head | (v << kMetaVShift) | (nsc == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
-           (vc ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (hi ? kMetaTopHi : 0u);
-  r.last_mask = kc == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
-  r.id = (uint32_t)(axc >> kJobLidShift4) & (uint32_t)(kJobPacketsW - 1);
-  r.B = r.ns - nsmax;
-  r.spread = nsmax - nsmin;
-  r.fast = !generic && r.ns <= kFastWMax && (r.ns == kRingW || r.spread <= 1);
-  return r;
-}
-
-// The ring of crc32_ragged16w_kernel: two positions of 2 KiB per wave (instruction 0's
-// 1 KiB, then instruction 1's kInstrStrideW further), in consumption order; the per-lane
-// offsets of the lane's two chunks inside a position; the landed data of the next slot.
-struct Ring2 {
-  uint32_t a0, a1;          // wave-uniform LDS byte addresses
-  uint32_t off_hi, off_lo;  // lane: chunk kc + 4 and chunk kc of its packet
-  u32x4 next_hi, next_lo;
-  template <int S>
-  __device__ __forceinline__ uint32_t at() const {
-    return S % 2 == 0 ? a0 : a1;
-  }
-  __device__ __forceinline__ uint32_t at_rt(uint32_t m) const { return m ? a1 : a0; }
-  __device__ __forceinline__ void rotate(uint32_t r) {
-    const uint32_t b0 = a0, b1 = a1;
-    a0 = r ? b1 : b0;
-    a1 = r ? b0 : b1;
-  }
-};
-
-// Wait until at most N DMAs are outstanding and read both chunks of the landed slot.
-template <int N>
-__device__ __forceinline__ void read_landed2(uint32_t addr_hi, uint32_t addr_lo, u32x4& hi, u32x4& lo) {
-  asm volatile(
-      "s_waitcnt vmcnt(%2)\n\t"
-      "ds_read_b128 %0, %3\n\t"
-      "ds_read_b128 %1, %4\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(hi), "=&v"(lo)
-      : "i"(N), "v"(addr_hi), "v"(addr_lo)
-      : "memory");
-}
-
-// h <- M(h) ^ w with the 16 lookups in one asm statement (no ring read).
-[[maybe_unused]] __device__ __forceinline__ void horner_step_lds(const Lookup& lk, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                                uint32_t& h3, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-  uint32_t a[16];
-  const uint32_t hs[4] = {h0, h1, h2, h3};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a[4 * j + t] = lookup_addr(hs[j], lk.lp, lk, t);
-  }
-  asm volatile(
-      "ds_read_b32 %4, %4\n\tds_read_b32 %5, %5\n\tds_read_b32 %6, %6\n\tds_read_b32 %7, %7\n\t"
-      "ds_read_b32 %8, %8\n\tds_read_b32 %9, %9\n\tds_read_b32 %10, %10\n\tds_read_b32 %11, %11\n\t"
-      "ds_read_b32 %12, %12\n\tds_read_b32 %13, %13\n\tds_read_b32 %14, %14\n\tds_read_b32 %15, %15\n\t"
-      "ds_read_b32 %16, %16\n\tds_read_b32 %17, %17\n\tds_read_b32 %18, %18\n\tds_read_b32 %19, %19\n\t"
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "v_bitop3_b32 %4, %4, %5, %6 bitop3:0x96\n\t"
-      "v_bitop3_b32 %0, %4, %7, %20 bitop3:0x96\n\t"
-      "v_bitop3_b32 %8, %8, %9, %10 bitop3:0x96\n\t"
-      "v_bitop3_b32 %1, %8, %11, %21 bitop3:0x96\n\t"
-      "v_bitop3_b32 %12, %12, %13, %14 bitop3:0x96\n\t"
-      "v_bitop3_b32 %2, %12, %15, %22 bitop3:0x96\n\t"
-      "v_bitop3_b32 %16, %16, %17, %18 bitop3:0x96\n\t"
-      "v_bitop3_b32 %3, %16, %19, %23 bitop3:0x96"
-      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]),
-        "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]),
-        "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
-      : "v"(w0), "v"(w1), "v"(w2), "v"(w3)
-      : "memory");
-}
-
-// h <- M(h) ^ w fused with the next slot's two ring reads (vmcnt(N) before them).
-template <int N>
-__device__ __forceinline__ void horner_step_and_read2(const Lookup& lk, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                                      uint32_t& h3, uint32_t w0, uint32_t w1, uint32_t w2,
-                                                      uint32_t w3, uint32_t addr_hi, uint32_t addr_lo, u32x4& nhi,
-                                                      u32x4& nlo) {
-  uint32_t a[16];
-  const uint32_t hs[4] = {h0, h1, h2, h3};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a[4 * j + t] = lookup_addr(hs[j], lk.lp, lk, t);
-  }
-  asm volatile(
-      "ds_read_b32 %6, %6\n\tds_read_b32 %7, %7\n\tds_read_b32 %8, %8\n\tds_read_b32 %9, %9\n\t"
-      "ds_read_b32 %10, %10\n\tds_read_b32 %11, %11\n\tds_read_b32 %12, %12\n\tds_read_b32 %13, %13\n\t"
-      "ds_read_b32 %14, %14\n\tds_read_b32 %15, %15\n\tds_read_b32 %16, %16\n\tds_read_b32 %17, %17\n\t"
-      "ds_read_b32 %18, %18\n\tds_read_b32 %19, %19\n\tds_read_b32 %20, %20\n\tds_read_b32 %21, %21\n\t"
-      "s_waitcnt vmcnt(%28)\n\t"
-      "ds_read_b128 %4, %22\n\t"
-      "ds_read_b128 %5, %23\n\t"
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "v_bitop3_b32 %6, %6, %7, %8 bitop3:0x96\n\t"
-      "v_bitop3_b32 %0, %6, %9, %24 bitop3:0x96\n\t"
-      "v_bitop3_b32 %10, %10, %11, %12 bitop3:0x96\n\t"
-      "v_bitop3_b32 %1, %10, %13, %25 bitop3:0x96\n\t"
-      "v_bitop3_b32 %14, %14, %15, %16 bitop3:0x96\n\t"
-      "v_bitop3_b32 %2, %14, %17, %26 bitop3:0x96\n\t"
-      "v_bitop3_b32 %18, %18, %19, %20 bitop3:0x96\n\t"
-      "v_bitop3_b32 %3, %18, %21, %27 bitop3:0x96"
-      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(nhi), "=&v"(nlo), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]),
-        "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]),
-        "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])
-      : "v"(addr_hi), "v"(addr_lo), "v"(w0), "v"(w1), "v"(w2), "v"(w3), "i"(N)
-      : "memory");
-}
-
-// A lane's Horner state: stream a (chunk kc of every 128-B piece) and, in the dual-stream
-// form, stream b (chunk kc + 4).  The single-stream form runs one M32^16 stream through
-// both chunks (b unused).
-struct HState {
-  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
-};
-
-// Dual-stream slot: a <- M32^32(a) ^ wa and b <- M32^32(b) ^ wb, the 32 lookups of both in
-// one LDS round trip, fused with the next slot's two ring reads (vmcnt(N) before them).
-template <int N>
-__device__ __forceinline__ void horner2_step_and_read2(const Lookup& lk, HState& h, uint32_t wa0, uint32_t wa1,
-                                                       uint32_t wa2, uint32_t wa3, uint32_t wb0, uint32_t wb1,
-                                                       uint32_t wb2, uint32_t wb3, uint32_t addr_hi, uint32_t addr_lo,
-                                                       u32x4& nhi, u32x4& nlo) {
-  uint32_t a[32];
-  const uint32_t hs[8] = {h.a0, h.a1, h.a2, h.a3, h.b0, h.b1, h.b2, h.b3};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a[4 * j + t] = lookup_addr(hs[j], lk.lp, lk, t);
-  }
-  asm volatile(
-      "ds_read_b32 %10, %10\n\tds_read_b32 %11, %11\n\tds_read_b32 %12, %12\n\tds_read_b32 %13, %13\n\t"
-      "ds_read_b32 %14, %14\n\tds_read_b32 %15, %15\n\tds_read_b32 %16, %16\n\tds_read_b32 %17, %17\n\t"
-      "ds_read_b32 %18, %18\n\tds_read_b32 %19, %19\n\tds_read_b32 %20, %20\n\tds_read_b32 %21, %21\n\t"
-      "ds_read_b32 %22, %22\n\tds_read_b32 %23, %23\n\tds_read_b32 %24, %24\n\tds_read_b32 %25, %25\n\t"
-      "ds_read_b32 %26, %26\n\tds_read_b32 %27, %27\n\tds_read_b32 %28, %28\n\tds_read_b32 %29, %29\n\t"
-      "ds_read_b32 %30, %30\n\tds_read_b32 %31, %31\n\tds_read_b32 %32, %32\n\tds_read_b32 %33, %33\n\t"
-      "ds_read_b32 %34, %34\n\tds_read_b32 %35, %35\n\tds_read_b32 %36, %36\n\tds_read_b32 %37, %37\n\t"
-      "ds_read_b32 %38, %38\n\tds_read_b32 %39, %39\n\tds_read_b32 %40, %40\n\tds_read_b32 %41, %41\n\t"
-      "s_waitcnt vmcnt(%52)\n\t"
-      "ds_read_b128 %8, %42\n\t"
-      "ds_read_b128 %9, %43\n\t"
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "v_bitop3_b32 %10, %10, %11, %12 bitop3:0x96\n\t"
-      "v_bitop3_b32 %0, %10, %13, %44 bitop3:0x96\n\t"
-      "v_bitop3_b32 %14, %14, %15, %16 bitop3:0x96\n\t"
-      "v_bitop3_b32 %1, %14, %17, %45 bitop3:0x96\n\t"
-      "v_bitop3_b32 %18, %18, %19, %20 bitop3:0x96\n\t"
-      "v_bitop3_b32 %2, %18, %21, %46 bitop3:0x96\n\t"
-      "v_bitop3_b32 %22, %22, %23, %24 bitop3:0x96\n\t"
-      "v_bitop3_b32 %3, %22, %25, %47 bitop3:0x96\n\t"
-      "v_bitop3_b32 %26, %26, %27, %28 bitop3:0x96\n\t"
-      "v_bitop3_b32 %4, %26, %29, %48 bitop3:0x96\n\t"
-      "v_bitop3_b32 %30, %30, %31, %32 bitop3:0x96\n\t"
-      "v_bitop3_b32 %5, %30, %33, %49 bitop3:0x96\n\t"
-      "v_bitop3_b32 %34, %34, %35, %36 bitop3:0x96\n\t"
-      "v_bitop3_b32 %6, %34, %37, %50 bitop3:0x96\n\t"
-      "v_bitop3_b32 %38, %38, %39, %40 bitop3:0x96\n\t"
-      "v_bitop3_b32 %7, %38, %41, %51 bitop3:0x96"
-      : "=&v"(h.a0), "=&v"(h.a1), "=&v"(h.a2), "=&v"(h.a3), "=&v"(h.b0), "=&v"(h.b1), "=&v"(h.b2), "=&v"(h.b3),
-        "=&v"(nhi), "=&v"(nlo), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
-        "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]), "+v"(a[14]),
-        "+v"(a[15]), "+v"(a[16]), "+v"(a[17]), "+v"(a[18]), "+v"(a[19]), "+v"(a[20]), "+v"(a[21]), "+v"(a[22]),
-        "+v"(a[23]), "+v"(a[24]), "+v"(a[25]), "+v"(a[26]), "+v"(a[27]), "+v"(a[28]), "+v"(a[29]), "+v"(a[30]),
-        "+v"(a[31])
-      : "v"(addr_hi), "v"(addr_lo), "v"(wa0), "v"(wa1), "v"(wa2), "v"(wa3), "v"(wb0), "v"(wb1), "v"(wb2), "v"(wb3),
-        "i"(N)
-      : "memory");
-}
-
-// The lane's top chunk (kc + 4 if kMetaTopHi, else kc) through its masks.
-[[maybe_unused]] __device__ __forceinline__ void mask_top_w(uint32_t meta, const TopMasks& m, uint32_t& x0, uint32_t& x1,
-                                           uint32_t& x2, uint32_t& x3, uint32_t& y0, uint32_t& y1, uint32_t& y2,
-                                           uint32_t& y3) {
-  if (meta & kMetaTopHi) {
-    x0 = and_xor(x0, m.am0, m.xm0);
-    x1 = and_xor(x1, m.am1, m.xm1);
-    x2 = and_xor(x2, m.am2, m.xm2);
-    x3 = and_xor(x3, m.am3, m.xm3);
-  } else {
-    y0 = and_xor(y0, m.am0, m.xm0);
-    y1 = and_xor(y1, m.am1, m.xm1);
-    y2 = and_xor(y2, m.am2, m.xm2);
-    y3 = and_xor(y3, m.am3, m.xm3);
-  }
-}
-
-// One slot of a fast round: refill this slot's ring position with slot S + 2 (two DMAs),
-// then the two Horner steps on the landed chunks (x = chunk kc + 4 first: it lies 64 B
-// below chunk kc in the packet), the second fused with the next slot's ring reads.  Lane
-// tops lie in slots B .. B + spread <= 1, issued by the previous round with per-lane
-// sources; slot B starts every stream (a stream is zero before its lane's top).
-template <int S, int NS, int B, bool kDual>
-__device__ __forceinline__ void roundw_slot(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                            const TopMasks& m, HState& h) {
-  constexpr int kF = S + kRingW;
-  const u32x4 vh = R.next_hi, vl = R.next_lo;
-  const uint32_t dst = R.at<S>();
-  if constexpr (kF < NS) {  // inside every packet of the round (kF > its top slot)
-    dma16(cur.cb0 + (uint64_t)kBytesPerStep * kF, dst);
-    dma16(cur.cb1 + (uint64_t)kBytesPerStep * kF, dst + kInstrStrideW);
-  } else {
-    dma16(srcw(nxt, 0, kF - NS, c.dummy), dst);
-    dma16(srcw(nxt, 1, kF - NS, c.dummy), dst + kInstrStrideW);
-  }
-  const uint32_t nb = R.at<S + 1>();
-  if constexpr (S < B) {
-    read_landed2<2 * (kRingW - 1)>(nb + R.off_hi, nb + R.off_lo, R.next_hi, R.next_lo);
-  } else {
-    uint32_t x0 = vh.x, x1 = vh.y, x2 = vh.z, x3 = vh.w;
-    uint32_t y0 = vl.x, y1 = vl.y, y2 = vl.z, y3 = vl.w;
-    if constexpr (S == NS - 1) y3 &= cur.last_mask;  // data only: before the injection
-    if constexpr (S < kRingW) {
-      if (NS == kRingW || S - B <= cur.spread) {
-        if (cur.top_slot == S) mask_top_w(cur.meta, m, x0, x1, x2, x3, y0, y1, y2, y3);
-      }
-    }
-    if constexpr (kDual) {
-      if constexpr (S == B) {  // M32^32(0) = 0: no lookups
-        h.a0 = y0;
-        h.a1 = y1;
-        h.a2 = y2;
-        h.a3 = y3;
-        h.b0 = x0;
-        h.b1 = x1;
-        h.b2 = x2;
-        h.b3 = x3;
-        read_landed2<2 * (kRingW - 1)>(nb + R.off_hi, nb + R.off_lo, R.next_hi, R.next_lo);
-      } else {
-        horner2_step_and_read2<2 * (kRingW - 1)>(c.lk, h, y0, y1, y2, y3, x0, x1, x2, x3, nb + R.off_hi,
-                                                 nb + R.off_lo, R.next_hi, R.next_lo);
-      }
-    } else {
-      if constexpr (S == B) {
-        h.a0 = x0;  // M32^16(0) = 0: no lookups
-        h.a1 = x1;
-        h.a2 = x2;
-        h.a3 = x3;
-      } else {
-        horner_step_lds(c.lk, h.a0, h.a1, h.a2, h.a3, x0, x1, x2, x3);
-      }
-      horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h.a0, h.a1, h.a2, h.a3, y0, y1, y2, y3, nb + R.off_hi,
-                                              nb + R.off_lo, R.next_hi, R.next_lo);
-    }
-  }
-  issue_order_fence();
-}
-
-template <int NS, int B, bool kDual, int... S>
-__device__ __forceinline__ void roundw_slots(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                             const TopMasks& m, HState& h, std::integer_sequence<int, S...>) {
-  (roundw_slot<S, NS, B, kDual>(cur, nxt, R, c, m, h), ...);
-}
-
-template <int NS, int B, bool kDual>
-__device__ __forceinline__ void roundw_fast(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                            HState& h) {
-  static_assert(B == 0 || NS == kRingW, "leading consumed slots only in ring-length rounds");
-  const TopMasks m = top_masks(cur.meta);
-  roundw_slots<NS, B, kDual>(cur, nxt, R, c, m, h, std::make_integer_sequence<int, NS>{});
-  R.rotate((uint32_t)(NS % 2));
-}
-
-// Any round (wider spreads, longer packets, chunks below the caller's buffer, a job's
-// partial last round): per-lane top slots and sources, runtime slot count.
-template <bool kDual>
-__device__ __forceinline__ void roundw_generic(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                               HState& h) {
-  const TopMasks tm = top_masks(cur.meta);
-  uint32_t m = 0;  // s % 2
-  for (int32_t s = 0; s < cur.ns; ++s) {
-    const u32x4 vh = R.next_hi, vl = R.next_lo;
-    const int32_t f = s + kRingW;
-    const uint32_t dst = R.at_rt(m);
-    if (f < cur.ns) {
-      dma16(srcw(cur, 0, f, c.dummy), dst);
-      dma16(srcw(cur, 1, f, c.dummy), dst + kInstrStrideW);
-    } else {
-      dma16(srcw(nxt, 0, f - cur.ns, c.dummy), dst);
-      dma16(srcw(nxt, 1, f - cur.ns, c.dummy), dst + kInstrStrideW);
-    }
-    m ^= 1u;
-    uint32_t x0 = vh.x, x1 = vh.y, x2 = vh.z, x3 = vh.w;
-    uint32_t y0 = vl.x, y1 = vl.y, y2 = vl.z, y3 = vl.w;
-    const bool top = s == cur.top_slot;
-    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
-      if (top && (cur.meta & kMetaFallback)) {
-        const uint64_t ca = cur.cbc + (uint64_t)kBytesPerStep * (uint64_t)s;
-        if (cur.meta & kMetaTopHi)
-          load_top_words(ca - 64u, cur.meta, c.dummy, x0, x1, x2, x3);
-        else
-          load_top_words(ca, cur.meta, c.dummy, y0, y1, y2, y3);
-      }
-    }
-    if (s == cur.ns - 1) y3 &= cur.last_mask;  // data only: before the injection
-    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
-      if (top) mask_top_w(cur.meta, tm, x0, x1, x2, x3, y0, y1, y2, y3);
-    }
-    const uint32_t nb = R.at_rt(m);
-    if constexpr (kDual) {
-      horner2_step_and_read2<2 * (kRingW - 1)>(c.lk, h, y0, y1, y2, y3, x0, x1, x2, x3, nb + R.off_hi, nb + R.off_lo,
-                                               R.next_hi, R.next_lo);
-    } else {
-      horner_step_lds(c.lk, h.a0, h.a1, h.a2, h.a3, x0, x1, x2, x3);
-      horner_step_and_read2<2 * (kRingW - 1)>(c.lk, h.a0, h.a1, h.a2, h.a3, y0, y1, y2, y3, nb + R.off_hi,
-                                              nb + R.off_lo, R.next_hi, R.next_lo);
-    }
-    issue_order_fence();
-  }
-  R.rotate(m);
-}
-
-template <bool kDual, int... I>
-__device__ __forceinline__ bool roundw_dispatch(const RoundW& cur, const RoundW& nxt, Ring2& R, const LaneConsts& c,
-                                                HState& h, std::integer_sequence<int, I...>) {
-  if (cur.ns == kRingW) {
-    if (cur.B == 0) roundw_fast<kRingW, 0, kDual>(cur, nxt, R, c, h);
-    else if (cur.B == 1) roundw_fast<kRingW, 1, kDual>(cur, nxt, R, c, h);
-    else return false;
-    return true;
-  }
-  return ((cur.ns == I + kRingW + 1 ? (roundw_fast<I + kRingW + 1, 0, kDual>(cur, nxt, R, c, h), true) : false) ||
-          ...);
-}
-
-// Dual-stream combine, valid on lane kc == 0: each stream's 4 words in-lane (M32^1), stream b
-// (chunks kc + 4: 16 words before stream a) through M32^16, then the 2-level tree M32^4, M32^8
-// across the packet's 4 lanes (fill_lds's tree tables).
-[[maybe_unused]] __device__ __forceinline__ uint32_t combine_dual(const uint32_t* lds, const HState& h, const Lookup& lk) {
-  uint32_t ya = apply_rep(lds, h.a0, h.a1, lk.lp1, lk);
-  uint32_t yb = apply_rep(lds, h.b0, h.b1, lk.lp1, lk);
-  ya = apply_rep(lds, ya, h.a2, lk.lp1, lk);
-  yb = apply_rep(lds, yb, h.b2, lk.lp1, lk);
-  ya = apply_rep(lds, ya, h.a3, lk.lp1, lk);
-  yb = apply_rep(lds, yb, h.b3, lk.lp1, lk);
-  uint32_t y = ya ^ apply_small(lds + kTreeDword + 2048, yb);
-  const uint32_t k = threadIdx.x & (kG4 - 1);
-  uint32_t t = 0;
-  if (k & 1u) t = apply_small(lds + kTreeDword, y);
-  y ^= from_lane_plus<1>(t);
-  if (k == 2u) t = apply_small(lds + kTreeDword + 1024, y);
-  y ^= from_lane_plus<2>(t);
-  return y;
-}
-
-template <bool kDual>
-__global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged16w_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
-  send_servers_home();
-  __shared__ __attribute__((aligned(16))) RaggedWLds<kDual> S;
-  uint32_t* const lds = S.tables;
-  constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
-  if (threadIdx.x < (unsigned)kJobSlotsW) {
-    S.ready[threadIdx.x] = 0;
-    S.consumed[threadIdx.x] = 0;
-    S.done[threadIdx.x] = 0;
-    S.freed[threadIdx.x] = 0;
-  }
-  if (threadIdx.x == 0) {
-    S.next_dispatch = kWavesPerBlock * kLook;
-    S.failed = 0;
-  }
-  if constexpr (kDual)
-    fill_lds(lds);
-  else
-    fill_lds4(lds);
-  __syncthreads();
-  const LaneConsts c = lane_consts(b.base);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t kc = lane & 3u, pc = lane >> 2, p8 = lane >> 3;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // fused lookups use raw addresses
-
-  auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
-  auto job_count = [&](uint64_t J) -> uint32_t {  // packets in job J (J < njobs)
-    const uint64_t left = b.count - J * kJobPacketsW;
-    return left < (uint64_t)kJobPacketsW ? (uint32_t)left : (uint32_t)kJobPacketsW;
-  };
-  auto round_valid = [&](uint32_t d) -> bool {
-    const uint64_t J = job_of(d >> 4);
-    return J < b.njobs && (d & 15u) * kPW4 < job_count(J);
-  };
-
-  // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0, u32
-  // lengths at +2048): three 16-B DMAs per lane, or, near the batch end, 12 4-B DMAs
-  // clamped to the batch.
-  auto job_dma = [&](uint64_t J, uint32_t slot) {
-    LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
-    const uint64_t p0 = J * kJobPacketsW;
-    if (p0 + kJobPacketsW <= b.count) {
-      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 2 * lane), (LdsVoid*)st, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 + 2 * lane), (LdsVoid*)(st + 1024), 16, 0,
-                                       0);
-      __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 4 * lane), (LdsVoid*)(st + 2048), 16, 0, 0);
-    } else {
-      const uint32_t* offw = reinterpret_cast<const uint32_t*>(b.offsets);
-#pragma unroll 1
-      for (uint32_t i = 0; i < 12; ++i) {
-        const uint32_t w = 64u * (i & 7u) + lane;
-        const uint64_t e = i < 8 ? p0 + w / 2 : p0 + 64u * (i - 8u) + lane;
-        const void* src = e >= b.count ? (const void*)g_zero_chunk
-                          : i < 8    ? (const void*)(offw + 2 * e + (w & 1u))
-                                     : (const void*)(b.lengths + e);
-        __builtin_amdgcn_global_load_lds(src, (LdsVoid*)(st + 256 * i), 4, 0, 0);
-      }
-    }
-  };
-  // Phase B (after a round body: every DMA but the last two has landed): sort the job's
-  // packets by 128-B step class (LDS histogram, as in crc32_ragged16_kernel), write its
-  // round records and headers in place of the descriptors, then mark the slot ready.
-  auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
-    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(2 * (kRingW - 1)) : "memory");
-    const uint32_t st = lds_addr(&S.job[slot].rec[0]);
-    const uint32_t hd = lds_addr(&S.job[slot].head[0]);
-    const uint32_t hi = lds_addr(&S.job[slot].hist[0]);
-    const uint32_t n = job_count(J);
-    uint32_t ln4;  // lane * 4 from asm: not hoisted out of the round loop
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 2, %0"
-                 : "=v"(ln4));
-    if (lane < 16u) {
-      lds_st32_nowait(hi + 4u * lane, 0u);
-      lds_st32_nowait(hd + 4u * lane, 0u);
-    }
-    const u32x4 o01 = lds_ld128(st + 8u * ln4), o23 = lds_ld128(st + 8u * ln4 + 16u);
-    const u32x4 ll = lds_ld128(st + 2048u + 4u * ln4);
-    const uint64_t off[4] = {o01.x | (uint64_t)o01.y << 32, o01.z | (uint64_t)o01.w << 32,
-                             o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
-    const uint32_t len[4] = {ll.x, ll.y, ll.z, ll.w};
-    uint64_t ax[4];
-    uint32_t info[4], cls[4], pos[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t id = ln4 + (uint32_t)i;
-      const bool v = id < n;
-      const RaggedRecord rec = ragged_record(b.base + off[i], len[i], c.base4);
-      ax[i] = v ? rec.ax | ((uint64_t)id << kJobLidShift4) : 0ull;
-      info[i] = rec.info;
-      const bool lng = rec.nsteps >= kClassLongW || ((rec.ax >> kRecNearBit) & 1u);
-      cls[i] = !v ? kClassNoneW : (lng ? kClassLongW : rec.nsteps);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pos[i] = lds_add_rtn(hi + 4u * cls[i], 1u);
-    uint32_t cnt = 0;
-    if (lane < 16u) cnt = lds_ld32(hi + 4u * lane);
-    const uint32_t first = wave_inclusive_add(cnt) - cnt;
-    if (lane < 16u) lds_st32(hi + 4u * lane, first);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t q = lds_ld32(hi + 4u * cls[i]) + pos[i];
-      const uint32_t r = st + (q >> 4) * kRoundWBytes;
-      lds_st64(r + 8u * (q & 15u), ax[i]);
-      lds_st32(r + 128u + 4u * (q & 15u), info[i]);
-      if (cls[i] != kClassNoneW) {
-        const uint32_t h = hd + 4u * (q >> 4);
-        const uint32_t ns8 = min(info[i] & kRecStepsMask, 255u);
-        if ((q & 15u) == 0u) lds_st8_nowait(h, ns8);
-        if ((q & 15u) == 15u || q + 1u == n) lds_st8_nowait(h + 1u, ns8);
-        // Longer packets, chunks near the caller's base, and the job's partial last round
-        // (its empty groups' chunk addresses lie below the base) take the generic body.
-        if (cls[i] == kClassLongW || ((q & 15u) != 15u && q + 1u == n)) lds_or_nowait(h, kHeadGeneric);
-      }
-    }
-    if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);  // waits for every LDS write above
-  };
-
-  // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
-  // (rounds 0 .. 31: jobs 0 and 1) and kJobAheadW more.
-  const uint32_t first_jobs = (kWavesPerBlock * kLook - 1) / kJobRoundsW + kJobAheadW + 1;
-  static_assert((kWavesPerBlock * kLook - 1) / kJobRoundsW + kJobAheadW + 1 <= kJobSlotsW, "prologue jobs");
-  if (wv < first_jobs && job_of(wv) < b.njobs) {
-    job_dma(job_of(wv), wv);
-    __builtin_amdgcn_s_waitcnt(0);
-    job_build(job_of(wv), wv, wv + 1u);
-  }
-  __syncthreads();
-
-  uint32_t seen_ready = 0, seen_freed = 0;
-  const uint32_t fail_a = lds_addr(&S.failed);
-  auto waited = [&](uint32_t w, uint32_t bit) -> bool {
-    if (w == kWaitGaveUp) report_fault(fail_a, bit);
-    return w == kWaitOk;
-  };
-  auto make_round = [&](uint32_t d) -> RoundW {
-    uint64_t axc = 0, ax0 = 0, ax1 = 0;
-    uint32_t ic = 0, i0 = 0, i1 = 0, hdr = 0;
-    const uint32_t k = d >> 4, slot = k & (uint32_t)(kJobSlotsW - 1), rj = d & 15u;
-    const uint64_t J = job_of(k);
-    const uint32_t n = J < b.njobs ? job_count(J) : 0u;
-    const bool live = rj * kPW4 < n;  // round_valid(d)
-    bool rv = live;
-    if (rv && k + 1u > seen_ready) {
-      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
-      if (rv) seen_ready = k + 1u;
-    }
-#ifdef ENET_CRC_TEST_HOOKS
-    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k) rv = waited(kWaitGaveUp, kFaultReady);
-#endif
-    if (rv) {
-      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + rj * kRoundWBytes;
-      asm volatile(
-          "ds_read_b64 %0, %7\n\tds_read_b32 %1, %8\n\t"
-          "ds_read_b64 %2, %9\n\tds_read_b32 %3, %10\n\t"
-          "ds_read_b64 %4, %11\n\tds_read_b32 %5, %12\n\t"
-          "ds_read_b32 %6, %13\n\ts_waitcnt lgkmcnt(0)"
-          : "=&v"(axc), "=&v"(ic), "=&v"(ax0), "=&v"(i0), "=&v"(ax1), "=&v"(i1), "=&v"(hdr)
-          : "v"(r + 8u * pc), "v"(r + 128u + 4u * pc), "v"(r + 8u * p8), "v"(r + 128u + 4u * p8),
-            "v"(r + 64u + 8u * p8), "v"(r + 160u + 4u * p8), "v"(lds_addr(&S.job[slot].head[rj]))
-          : "memory");
-      hdr = __builtin_amdgcn_readfirstlane(hdr);
-      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
-    }
-    RoundW rr = roundw_from_records(axc, ic, ax0, i0, ax1, i1, rv, hdr, c);
-    rr.live = live;
-    rr.job_k = k;
-    rr.job_rounds = (n + kPW4 - 1) / kPW4;
-    return rr;
-  };
-
-  uint32_t rnd1 = wv + kWavesPerBlock;
-  if (!round_valid(wv)) return;
-  RoundW cur = make_round(wv);
-  RoundW nxt = make_round(rnd1);
-  Ring2 R;
-  R.a0 = lds_addr(&S.ring[0][0][wv][0]);
-  R.a1 = lds_addr(&S.ring[1][0][wv][0]);
-  R.off_lo = (pc >> 3) * kInstrStrideW + 16u * (8u * (pc & 7u) + kc);
-  R.off_hi = R.off_lo + 64u;
-  dma16(srcw(cur, 0, 0, c.dummy), R.a0);  // cur.ns >= kRingW
-  dma16(srcw(cur, 1, 0, c.dummy), R.a0 + kInstrStrideW);
-  dma16(srcw(cur, 0, 1, c.dummy), R.a1);
-  dma16(srcw(cur, 1, 1, c.dummy), R.a1 + kInstrStrideW);
-  read_landed2<2 * (kRingW - 1)>(R.a0 + R.off_hi, R.a0 + R.off_lo, R.next_hi, R.next_lo);
-  while (cur.live) {
-    uint32_t d = 0;
-    if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
-    d = __builtin_amdgcn_readfirstlane(d);
-    // Build duty: the claimer of a job's first round builds the job kJobAheadW later once
-    // every round of the slot's previous job has read its record (crc32_ragged_jobs_kernel).
-    bool build = false;
-    const uint32_t kb = (d >> 4) + kJobAheadW, bslot = kb & (uint32_t)(kJobSlotsW - 1);
-    if ((d & 15u) == 0u && kb >= first_jobs && job_of(kb) < b.njobs) {
-      build = kb < (uint32_t)kJobSlotsW ||
-              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), kJobRoundsW, fail_a), kFaultConsumed);
-      if (build) {
-        if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
-        job_dma(job_of(kb), bslot);
-      }
-    }
-    HState h = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (!cur.fast || !roundw_dispatch<kDual>(cur, nxt, R, c, h, std::make_integer_sequence<int, kFastWMax - kRingW>{}))
-      roundw_generic<kDual>(cur, nxt, R, c, h);
-    uint32_t y;
-    if constexpr (kDual)
-      y = combine_dual(lds, h, c.lk);
-    else
-      y = combine_tree4(lds, h.a0, h.a1, h.a2, h.a3, c.lk);
-    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane kc == 0 holds it
-    if (cur.meta & kMetaEmpty) reg = kInitRegister;
-    const uint32_t k0 = cur.job_k, slot0 = k0 & (uint32_t)(kJobSlotsW - 1);
-    if (k0 >= (uint32_t)kJobSlotsW && k0 + 1u - (uint32_t)kJobSlotsW > seen_freed) {
-      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlotsW + 1u, fail_a), kFaultFreed))
-        seen_freed = k0 + 1u - (uint32_t)kJobSlotsW;
-    }
-    if (kc == 0 && (cur.meta & kMetaStore))
-      lds_st32_nowait(lds_addr(&S.job[slot0].res[cur.id]), __builtin_bswap32(~reg));
-    uint32_t old = 0;
-    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old + 1u == cur.job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
-      const uint64_t J0 = job_of(k0);
-      const uint32_t n0 = job_count(J0);
-      const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
-      uint32_t* dst = out + J0 * kJobPacketsW + 4u * lane;
-      if (4u * lane + 4u <= n0) {
-        reinterpret_cast<U32x4A4*>(dst)->v = v;
-      } else {
-        if (4u * lane + 0u < n0) dst[0] = v.x;
-        if (4u * lane + 1u < n0) dst[1] = v.y;
-        if (4u * lane + 2u < n0) dst[2] = v.z;
-      }
-    }
-    if (old + 1u == cur.job_rounds && lane == 0) {
-      lds_st32(lds_addr(&S.done[slot0]), 0u);
-      lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
-    }
-    if (build) job_build(job_of(kb), bslot, kb + 1u);
-    const RoundW after = make_round(d);
-    cur = nxt;
-    nxt = after;
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-}
-
-#endif  // 16-packet-round measurement builds
 
 }  // namespace
 
@@ -3735,18 +2262,11 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // In-kernel job sort (crc32_ragged_jobs_kernel; the 16-packet-round crc32_ragged16_kernel
-  // in the ENET_CRC_RAGGED16 measurement build: slower): one launch, no scratch.  Workgroups take jobs statically,
+  // In-kernel job sort (crc32_ragged_jobs_kernel): one launch, no scratch.  Workgroups take jobs statically,
   // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
   // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
   // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
-#if defined(ENET_CRC_RAGGED16W) || defined(ENET_CRC_RAGGED16D)  // fixed jobs of 16 rounds (the kernel's d >> 4)
-  constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRoundsW, kMinJobRounds = kJobRoundsW;
-#elif defined(ENET_CRC_RAGGED16)
-  constexpr uint64_t kRoundPackets = kPW4, kMaxJobRounds = kJobRounds4, kMinJobRounds = kJobRounds4 / 2;
-#else
   constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds, kMinJobRounds = kJobRounds / 2;
-#endif
   const int cus = cu_count_for_current_device();
   if (cus <= 0) return hipErrorNoDevice;
   uint64_t jp = kMaxJobRounds * kRoundPackets, njobs = 0, best = ~0ull;
@@ -3780,15 +2300,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
   jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
 #endif
-#if defined(ENET_CRC_RAGGED16D)
-  hipLaunchKernelGGL(crc32_ragged16w_kernel<true>, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
-#elif defined(ENET_CRC_RAGGED16W)
-  hipLaunchKernelGGL(crc32_ragged16w_kernel<false>, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
-#elif defined(ENET_CRC_RAGGED16)
-  hipLaunchKernelGGL(crc32_ragged16_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
-#else
   hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
-#endif
   return hipGetLastError();
 }
 

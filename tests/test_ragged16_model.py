@@ -1,8 +1,9 @@
 """Host model of the ragged kernels' addressing (rusty_enet_amd/csrc/crc32_kernels.hip): the
 product's crc32_ragged_jobs_kernel (8 lanes x 128-B pieces per packet, 8 packets per round,
-ring of 3), and the measurement builds crc32_ragged16_kernel (4 lanes x 64-B pieces, 16
-packets per round) and crc32_ragged16w_kernel (16 packets loaded as 8 lanes x 128-B pieces,
-two DMA instructions per slot, ring of 2).  Job partition, per-packet records (ragged_record4 / ragged_record), the
+ring of 3), and the round-4 measurement builds crc32_ragged16_kernel (4 lanes x 64-B pieces,
+16 packets per round) and crc32_ragged16w_kernel (16 packets loaded as 8 lanes x 128-B
+pieces, two DMA instructions per slot, ring of 2), parked in
+profiles/r04/parked/round4_measurement_builds.patch.  Job partition, per-packet records (ragged_record4 / ragged_record), the
 class sort and round headers of the job build, each DMA lane's round plan
 (round16_from_record / dma_plan_w) and the source of every LDS-DMA the round bodies issue.
 No GPU.
