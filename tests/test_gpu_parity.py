@@ -293,15 +293,16 @@ def test_ragged_region_sort_edges(dev, count):
 
 
 @pytest.mark.parametrize("shape", ["near_base", "wide_spread", "tiny", "long_mix", "mtu_unaligned", "one_job"])
-def test_ragged16_round_paths(dev, shape):
-    """The round bodies of crc32_ragged16_kernel (16 packets per round, 64-B steps):
-    near_base: overlapping packets starting in the first 16 bytes of the buffer (top chunks
-    that would reach below it: the generic body's fallback loads); wide_spread: six step
-    classes far apart, so the rounds where classes meet differ by > 2 steps (generic body);
-    tiny: packets of <= 3 steps at every alignment (ring-length rounds, first top slot
-    0, 1 or 2); long_mix: packets of 23+ steps (the longer class, generic) next to short
-    ones; mtu_unaligned: 1392-B datagrams from base + 1 (the frag_64k shape); one_job: a
-    batch of one partial job per workgroup."""
+def test_ragged_round_paths(dev, shape):
+    """The round bodies of crc32_ragged_jobs_kernel (8 packets per round, 128-B steps; first
+    written for the parked 16-packet kernel): near_base: overlapping packets starting in the
+    first 16 bytes of the buffer (top chunks that would reach below it: the generic body's
+    fallback loads); wide_spread: six step classes far apart, so the rounds where classes
+    meet differ by > 1 step (generic body); tiny: packets of <= 3 steps at every alignment
+    (ring-length rounds, top slots 0, 1 and 2 mixed in one unrolled body); long_mix: packets
+    of 15+ steps (the longer class, generic) next to short ones; mtu_unaligned: 1392-B
+    datagrams from base + 1 (the frag_64k shape); one_job: a batch of one partial job per
+    workgroup."""
     rng = np.random.default_rng(zlib.crc32(shape.encode()))
     n = 9000
     if shape == "near_base":
