@@ -645,6 +645,10 @@ struct UniformBatch {
   uint64_t stride;
   uint32_t length;
   uint64_t count;
+  // crc32_uniform_regs_kernel only: packets p >= skip_at are packets p + skip of the batch
+  // (address and output), so one launch covers a head and a tail around a whole-line run.
+  uint64_t skip_at = ~0ull;
+  uint64_t skip = 0;
 };
 
 // ---------------------------------------------------------------------------------
@@ -1218,9 +1222,10 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
   const bool none0 = rel0 <= -16;
   const bool part0 = rel0 < 0 && rel0 > -16;
   const uint32_t head_meta = part0 ? (uint32_t)(rel0 / 4 + 4) : 0u;
+  auto batch_index = [&](uint64_t p) -> uint64_t { return p + (p >= u.skip_at ? u.skip : 0u); };
   auto packet_base = [&](uint64_t rnd) -> uint64_t {
     const uint64_t p = rnd * kPacketsPerWave + c.grp;
-    return u.base + (p < u.count ? p : u.count - 1) * u.stride;
+    return u.base + batch_index(p < u.count ? p : u.count - 1) * u.stride;
   };
   auto is_below = [&](uint64_t pb) -> bool { return part0 && (int64_t)(pb - u.base) + rel0 < 0; };
   auto slot_src = [&](uint64_t pb, int32_t s) -> uint64_t {
@@ -1293,7 +1298,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_regs_kernel(UniformBatch
     rnd1 = round_of(__builtin_amdgcn_readfirstlane(d));
     if (j == 7u || rnd0 >= total_rounds) {
       const uint64_t p = res_round * kPacketsPerWave + c.grp;
-      if (c.k <= j && p < u.count) out[p] = res;
+      if (c.k <= j && p < u.count) out[batch_index(p)] = res;
       j = 0;
     } else {
       ++j;
@@ -2202,25 +2207,19 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t length,
       const bool lines = lines_shape(b0, stride, length, head);
       const uint64_t whole = lines && count > head ? (count - head) / kPacketsPerWave * kPacketsPerWave : 0;
       if (lines && nsl >= kUniformRing && nsl <= kMaxRoundSteps && whole > 0) {
-        if (head > 0) {
-          const UniformBatch h{b0, stride, length, head};
-          const unsigned hblocks = grid_for(head, err);
-          if (err != hipSuccess) return err;
-          err = dispatch_uniform_regs(nsx, h, out, stream, hblocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
-          if (err != hipSuccess) return err;
-        }
         const UniformBatch w{b0 + head * stride, stride, length, whole};
         const unsigned wblocks = grid_for(whole, err);
         if (err != hipSuccess) return err;
         err = dispatch_uniform_lines(nsl, w, out + head, stream, wblocks,
                                      std::make_integer_sequence<int, kMaxRoundSteps - kUniformRing + 1>{});
-        const uint64_t done = head + whole;
-        if (err != hipSuccess || done == count) return err;
-        const UniformBatch t{b0 + done * stride, stride, length, count - done};
-        const unsigned tblocks = grid_for(count - done, err);
+        const uint64_t rest = count - whole;  // the head and the tail: one launch
+        if (err != hipSuccess || rest == 0) return err;
+        UniformBatch t{b0, stride, length, rest};
+        t.skip_at = head;
+        t.skip = whole;
+        const unsigned tblocks = grid_for(rest, err);
         if (err != hipSuccess) return err;
-        return dispatch_uniform_regs(nsx, t, out + done, stream, tblocks,
-                                     std::make_integer_sequence<int, kMaxRoundSteps>{});
+        return dispatch_uniform_regs(nsx, t, out, stream, tblocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
       }
       return dispatch_uniform_regs(nsx, u, out, stream, blocks, std::make_integer_sequence<int, kMaxRoundSteps>{});
     }
