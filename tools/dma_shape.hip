@@ -12,6 +12,7 @@
 //   4x256x1 d2/3 16 lanes per packet (256-B pieces of 4 packets)
 //   2x512x1 d2   32 lanes per packet
 //   16x128x2 d1  two 8x128 instructions per slot, one slot in flight
+//   8x128 regs   the 8-lane shape loaded into a register ring (3 or 6 deep; nt: non-temporal)
 // Workgroups of 1024 threads, one per CU (the LDS is padded to the kernels' 150 KiB), a
 // persistent grid over static rounds.  Alternating blocks of 20 launches per shape after a
 // warm-up; prints us per launch and GB/s.  Addresses stay inside the buffer: the packets
@@ -107,11 +108,67 @@ __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32
   out[(blockIdx.x * 1024 + threadIdx.x)] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
+// The same walk with the pieces loaded into a register ring (global_load_dwordx4, D slots
+// deep, optionally non-temporal) instead of LDS-DMA: the G1 kernel's load form.
+template <int P, int PIECE, int D, bool kNT>
+__global__ __launch_bounds__(1024) void shape_regs_kernel(const uint8_t* base, uint32_t L, uint64_t rounds,
+                                                          uint64_t amask, uint32_t* out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];  // same occupancy as the DMA form
+  constexpr int kLanesPerPkt = PIECE / 16;
+  static_assert(P * PIECE == 1024, "one instruction per slot");
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t ns = (L + PIECE - 1) / PIECE;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wv, nw = (uint64_t)gridDim.x * kWaves;
+  const uint64_t my_rounds = gw < rounds ? (rounds - gw + nw - 1) / nw : 0;
+  if (my_rounds == 0) return;
+  const uint64_t q_end = my_rounds * ns;
+  const uint64_t last_round = my_rounds - 1;
+  const uint32_t pkt = lane / kLanesPerPkt, k = lane % kLanesPerPkt;
+  auto src = [&](uint64_t j, uint32_t s) -> const u32x4* {
+    const uint64_t r = gw + j * nw;
+    const uint8_t* end = base + (r * P + pkt + 1) * (uint64_t)L;
+    return (const u32x4*)((((uint64_t)(end - (uint64_t)PIECE * (ns - s))) & amask) + 16 * k);
+  };
+  uint64_t dj = 0;
+  uint32_t dsl = 0;
+  auto advance = [&]() {
+    if (dj == last_round && dsl == ns - 1) return;
+    if (++dsl == ns) {
+      dsl = 0;
+      ++dj;
+    }
+  };
+  u32x4 ring[D];
+  u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    ring[d] = kNT ? __builtin_nontemporal_load(src(dj, dsl)) : *src(dj, dsl);
+    advance();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (uint64_t q = 0; q + D <= q_end + D - 1; q += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc ^= ring[d];
+      ring[d] = kNT ? __builtin_nontemporal_load(src(dj, dsl)) : *src(dj, dsl);
+      advance();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (lane == 0) lds[wv] = (uint8_t)acc.x;
+  out[(blockIdx.x * 1024 + threadIdx.x)] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
 struct Shape {
   const char* name;
   int P;
   void (*launch)(int grid, const uint8_t*, uint32_t, uint64_t, uint64_t, uint32_t*);
 };
+
+template <int P, int PIECE, int D, bool kNT>
+void launch_regs(int grid, const uint8_t* b, uint32_t L, uint64_t rounds, uint64_t amask, uint32_t* out) {
+  hipLaunchKernelGGL((shape_regs_kernel<P, PIECE, D, kNT>), dim3(grid), dim3(1024), 0, 0, b, L, rounds, amask, out);
+}
 
 template <int P, int PIECE, int I, int D>
 void launch_shape(int grid, const uint8_t* b, uint32_t L, uint64_t rounds, uint64_t amask, uint32_t* out) {
@@ -144,6 +201,8 @@ int main(int argc, char** argv) {
       {"8x128x1 d2", 8, launch_shape<8, 128, 1, 2>},   {"4x256x1 d2", 4, launch_shape<4, 256, 1, 2>},
       {"4x256x1 d3", 4, launch_shape<4, 256, 1, 3>},   {"2x512x1 d2", 2, launch_shape<2, 512, 1, 2>},
       {"16x128x2 d1", 16, launch_shape<16, 128, 2, 1>},
+      {"8x128 regs d3", 8, launch_regs<8, 128, 3, false>}, {"8x128 regs d6", 8, launch_regs<8, 128, 6, false>},
+      {"8x128 regsnt d6", 8, launch_regs<8, 128, 6, true>},
   };
   const int ns = sizeof(shapes) / sizeof(shapes[0]);
   hipDeviceProp_t prop;
