@@ -330,6 +330,35 @@ def test_ragged_round_paths(dev, shape):
     assert np.array_equal(got, want), int(np.count_nonzero(got != want))
 
 
+@pytest.mark.parametrize("mix", ["adjacent_classes", "empties_in_short_rounds", "class_pairs_every_round"])
+def test_ragged_mixed_class_rounds(dev, mix):
+    """Rounds whose packets' top slots differ, all in the unrolled bodies since round 4
+    (round_from_record: top slots in B .. B + 1, any in ring-length rounds):
+    adjacent_classes: lengths at both sides of 128-B step boundaries, so sorted rounds straddle
+    two classes (top slots 0 and 1) at every alignment; empties_in_short_rounds: zero-length
+    packets among 1-3-step ones (ring-length rounds whose empty groups never read);
+    class_pairs_every_round: 4 packets of each of two adjacent classes per 8, so nearly every
+    round mixes (plus a few 3-class rounds, the generic body)."""
+    rng = np.random.default_rng(zlib.crc32(mix.encode()))
+    n = 12000
+    if mix == "adjacent_classes":
+        edge = rng.integers(2, 11, size=n) * 128
+        lengths = (edge + rng.integers(-20, 21, size=n)).astype(np.uint32)
+    elif mix == "empties_in_short_rounds":
+        lengths = np.where(rng.random(n) < 0.3, 0, rng.integers(1, 384, size=n)).astype(np.uint32)
+    else:
+        pair = rng.integers(1, 10, size=n // 8)
+        lengths = np.concatenate([np.concatenate([rng.integers(128 * p - 100, 128 * p + 1, size=4),
+                                                  rng.integers(128 * p + 1, 128 * p + 100, size=4)])
+                                  for p in pair]).astype(np.uint32)
+    offsets = (packed_offsets(lengths) + np.cumsum(rng.integers(0, 4, size=lengths.size))).astype(np.uint64)
+    offsets += np.uint64(2)
+    data = splitmix64_bytes(63 + len(mix), int(offsets[-1] + lengths[-1]) + 8)
+    got = ragged_on_device(data, offsets, lengths, dev)
+    want = _oracle.crc32_ragged(data, offsets, lengths)
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+
+
 # --- round-record scratch cached per stream (launch_ragged) ----------------------------------
 
 def test_ragged_scratch_per_stream(dev):

@@ -162,7 +162,11 @@ def _shape(name: str):
                 lens.append(ln)
                 pos += ln
         return np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
-    if name == "wide_spread":
+    if name == "adjacent_classes":  # sorted rounds straddling two 128-B step classes
+        lengths = (rng.integers(2, 11, size=n) * 128 + rng.integers(-20, 21, size=n)).astype(np.uint32)
+    elif name == "empties_short":  # zero-length packets among 1-3-step ones
+        lengths = np.where(rng.random(n) < 0.3, 0, rng.integers(1, 384, size=n)).astype(np.uint32)
+    elif name == "wide_spread":
         lengths = rng.choice(np.array([40, 300, 560, 820, 1080, 1340], dtype=np.uint32), size=n)
     elif name == "tiny":
         lengths = rng.integers(0, 193, size=n).astype(np.uint32)
@@ -180,7 +184,7 @@ def _shape(name: str):
 
 @pytest.mark.parametrize("kernel", sorted(KERNELS))
 @pytest.mark.parametrize("name", ["g2", "frag", "near_base", "every_length", "wide_spread", "tiny", "long_mix",
-                                  "edges", "one_job"])
+                                  "edges", "one_job", "adjacent_classes", "empties_short"])
 def test_ragged16_addresses(kernel, name):
     offsets, lengths = _shape(name)
     stats = check_batch(KERNELS[kernel], offsets, lengths)
