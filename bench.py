@@ -421,6 +421,103 @@ def ring_rate(dev, L: int = 1200, nslots: int = 4, per_slot: int = 40000, rounds
             "sample": f"{nslots} pinned slots x {per_slot} x {L} B, {rounds} rounds of submit-all/wait-all"}
 
 
+VERIFY_BATCHES = (16, 32, 64, 128, 256, 512, 1024, 4096, 16384)
+
+
+def verify_batch(dev, batch: int = 256, reps: int = 200) -> dict:
+    """The receive path at the reference's own batch size: enet_protocol_receive_incoming_commands
+    takes at most 256 datagrams per service() (src/c/protocol.rs:1655) and checksums each one
+    as it handles it (:1470-1502).  Per-batch microseconds for B ragged datagrams of U{64..1392}
+    B from host memory: enet_crc32_ragged_host (pageable, staged through pinned memory) plus
+    the per-datagram slot correction (enet_crc32_slot_adjust, as the receive loop would call it);
+    one pinned ring slot (submit + wait); the whole Python mirror protocol.verify_received; and
+    the reference's cost, B calls of the C restatement of src/crc32.rs on one core.  Each GPU
+    path is checked bit-exact against the oracle first; the crossover is the smallest batch
+    in VERIFY_BATCHES at which the host path beats the one-core CPU."""
+    import ctypes
+
+    import _oracle
+    from _data import ENET_SEED, packed_offsets, ragged_lengths, splitmix64_bytes
+
+    import rusty_enet_amd as rea
+    from rusty_enet_amd import _native, protocol
+    from rusty_enet_amd.ring import ReceiveRing
+
+    def med(fn, k):
+        fn()
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e6
+
+    def sample(b, seed):
+        ln = ragged_lengths(ENET_SEED + seed, b, lo=64, hi=1392)
+        off = packed_offsets(ln)
+        return splitmix64_bytes(ENET_SEED + seed + 1, int(ln.sum())), off, ln
+
+    lib = _native.lib()
+    adj = lib.enet_crc32_slot_adjust
+    ctx = rea.Context(dev.index or 0)
+    rows = {}
+    for b in sorted(set(VERIFY_BATCHES) | {batch}):
+        data, off, ln = sample(b, 300 + b)
+        want = _oracle.crc32_ragged(data, off, ln)
+        if not np.array_equal(ctx.crc32_ragged_host(data, off, ln), want):
+            raise SystemExit(f"bench: {b}-datagram host batch differs from the oracle")
+        out = np.empty(b, dtype=np.uint32)
+        args = (ctx.handle, data.ctypes.data, off.ctypes.data, ln.ctypes.data, b, out.ctypes.data)
+        host_us = med(lambda: lib.enet_crc32_ragged_host(*args), reps)
+        cpu_us = med(lambda: _oracle.crc32_ragged(data, off, ln), reps)  # one C loop over B datagrams
+        rows[b] = {"host_us": round(host_us, 1), "cpu_1core_us": round(cpu_us, 1),
+                   "bytes": int(ln.sum())}
+    data, off, ln = sample(batch, 300 + batch)
+    crcs = ctx.crc32_ragged_host(data, off, ln)
+    # the receive loop's slot correction (connect_id instead of the wire value), in C per datagram
+    slot_us = med(lambda: [adj(int(c), 0x11223344, 0x55667788, int(n) - 6) for c, n in zip(crcs, ln)], 20)
+    call_us = med(lambda: [adj(1, 2, 3, 4) for _ in range(batch)], 20)  # the ctypes call alone
+    with ReceiveRing(dev.index or 0, nslots=1, slot_bytes=batch * 1392, slot_packets=batch) as ring:
+        r_data, r_off, r_ln, r_crc = ring.slot(0)
+        r_data[:data.size] = data
+        r_off[:batch] = off
+        r_ln[:batch] = ln
+        ring.submit(0, batch)
+        ring.wait(0)
+        if not np.array_equal(r_crc[:batch], crcs):
+            raise SystemExit("bench: ring slot checksums differ")
+        ring_us = med(lambda: (ring.submit(0, batch), ring.wait(0)), reps)
+    dgrams = [bytes(data[int(o):int(o) + int(n)]) for o, n in zip(off, ln)]
+    # datagrams as a client with peer id 7 sends them: the slot holds the checksum with the
+    # connect_id in it, so every one is accepted
+    conn = 0x0BADF00D
+    dg = []
+    for d in dgrams:
+        a = bytearray(d)
+        a[0], a[1] = 0x00, 0x07  # peer id 7, no flags: header 2 + 4
+        dg.append(a)
+    protocol.insert_outgoing(dg, [2] * batch, [conn] * batch, ctx=ctx)
+    ok = protocol.verify_received(dg, lambda pid: conn, ctx=ctx)
+    if not all(ok):
+        raise SystemExit("bench: verify_received rejected a valid datagram")
+    proto_us = med(lambda: protocol.verify_received(dg, lambda pid: conn, ctx=ctx), 50)
+    ctx.close()
+    cross = next((b for b in sorted(rows) if rows[b]["host_us"] < rows[b]["cpu_1core_us"]), None)
+    r = rows[batch]
+    return {"batch": batch, "unit": "us per batch",
+            "host_us": r["host_us"], "slot_adjust_us": round(max(slot_us - call_us, 0.0), 1),
+            "ring_us": round(ring_us, 1), "cpu_1core_us": r["cpu_1core_us"],
+            "protocol_verify_received_us": round(proto_us, 1), "bytes": r["bytes"],
+            "crossover_batch": cross,
+            "sweep": {str(b): rows[b] for b in sorted(rows)},
+            "sample": f"{batch} datagrams of U{{64..1392}} B (the reference's receive batch, src/c/protocol.rs:1655), "
+                      f"median of {reps}; host: enet_crc32_ragged_host from pageable memory; slot_adjust: "
+                      f"{batch} enet_crc32_slot_adjust calls less the ctypes call cost; ring: one pinned ring slot "
+                      "submit + wait; protocol: the Python mirror verify_received (header parse, one GPU pass, "
+                      "per-datagram correction); cpu: the C restatement of src/crc32.rs over the same datagrams on "
+                      "one core; crossover: smallest batch of the sweep where host_us < cpu_1core_us"}
+
+
 # --------------------------------------------------------------------------------------
 # roofline evidence
 # --------------------------------------------------------------------------------------
@@ -810,6 +907,7 @@ def main(argv=None) -> int:
             line["cpu_baseline"] = range_cpu_baseline(spec) if is_range else cpu_baseline(args.cpu_seconds)
         if world == 1 and not args.no_e2e and not is_range:
             line["end_to_end"] = end_to_end(dev)
+            line["verify_256"] = verify_batch(dev)
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.barrier()

@@ -75,9 +75,10 @@ typedef struct enet_crc_ctx enet_crc_ctx;
  * the batched receive verify / send insert below (INTEGRATION.md §3 is the recommended
  * integration), at ~5 TB/s on the device.
  */
-#define ENET_CRC_PERCALL_COPY 0     /* pinned staging -> H2D copy -> kernel -> D2H copy (~20 us) */
+#define ENET_CRC_PERCALL_COPY 0     /* pinned staging -> H2D copy -> kernel -> D2H copy (~24 us) */
 /* (default) One single-packet launch that reads the gathered bytes from mapped pinned
- * memory and writes the result to mapped memory; nothing stays resident (~17-19 us). */
+ * memory and writes the result to mapped memory; nothing stays resident (~21 us through
+ * ctypes on the round-4 box). */
 #define ENET_CRC_PERCALL_ZEROCOPY 1
 /* Opt-in.  A server wave stays resident on lane 0's device and polls a request mailbox
  * (device memory the host writes through the PCIe BAR on large-BAR devices, else pinned
@@ -96,7 +97,13 @@ typedef struct enet_crc_ctx enet_crc_ctx;
 
 /* ENET_CRC_ABI_VERSION: 4 added enet_crc32_combine; 5 added enet_crc_ctx_percall_mode and
  * enet_crc_ctx_stop_server and made ZEROCOPY the default per-call mode; 6 added
- * ENET_CRC_E_DEVICE and enet_crc_device_status.  Nothing was removed. */
+ * ENET_CRC_E_DEVICE and enet_crc_device_status.  Nothing was removed.  Behaviour changes
+ * within ABI 6: enet_crc32_shards_device checks placement and rejects buffers that are not
+ * device memory of the shard's device (mapped pinned host memory and managed memory, which
+ * it used to read over the fabric, now return ENET_CRC_E_INVALID); enet_crc_ctx_stop_server
+ * returns ENET_CRC_E_HIP (hipErrorLaunchTimeOut) when the server wave does not stop; the
+ * synchronous entries report only their own launches' failures (per-slot failure words)
+ * and no longer read or clear the device word. */
 ENET_CRC_API int enet_crc_abi_version(void);
 ENET_CRC_API const char* enet_crc_strerror(int status);
 /* hipError_t of the last failing HIP call made by this thread (0 if none). */
@@ -109,14 +116,17 @@ ENET_CRC_API int enet_crc_device_count(void);
  * flags in LDS; a wait that does not complete within its poll limit (never observed:
  * DESIGN.md §4) is given up rather than left to hang the GPU.  The wave that gives up
  * writes a failure bit (1: a job's records never became ready, 2: a job slot was never
- * released, 4: a result slot was never flushed) into the device's failure word, and its
- * workgroup stops writing checksums.  The word is per device and sticky:
+ * released, 4: a result slot was never flushed) into the failure word its launch carries,
+ * and its workgroup stops writing checksums.  Words are sticky until cleared:
  *   - the synchronous entries (enet_crc32_ragged_host, enet_crc_ring_wait, and the
- *     receive/send loops built on them) check it after their last wait; if it is set they
- *     clear it and return ENET_CRC_E_DEVICE: no output of that call may be trusted;
- *   - after the asynchronous *_device entries, synchronise the stream and call
- *     enet_crc_device_status(device, clear): > 0 means some batch on that device since
- *     the last clear produced invalid outputs.
+ *     receive/send loops built on them) give every staging / ring slot a word of its own,
+ *     cleared before the slot's launches and read after the call's last wait: such a call
+ *     returns ENET_CRC_E_DEVICE exactly when one of its own launches failed (no output of
+ *     that call may be trusted), whatever else runs on the device;
+ *   - the asynchronous *_device entries report into the device's word: synchronise the
+ *     stream and call enet_crc_device_status(device, clear): > 0 means some asynchronous
+ *     batch on that device since the last clear produced invalid outputs (the word is
+ *     shared by every asynchronous caller on the device).
  * Returns the bits (0 = no failure), or a negative status for a bad device.
  */
 ENET_CRC_API int enet_crc_device_status(int device, int clear);
@@ -144,7 +154,9 @@ ENET_CRC_API int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode);
 /* The context's current per-call mode (ENET_CRC_PERCALL_*), or ENET_CRC_E_INVALID. */
 ENET_CRC_API int enet_crc_ctx_percall_mode(enet_crc_ctx* ctx);
 /* Stop the context's persistent server wave now, if one runs (the next persistent-mode
- * call relaunches it).  Call before a device-wide synchronisation. */
+ * call relaunches it).  Call before a device-wide synchronisation.  ENET_CRC_E_HIP
+ * (hipErrorLaunchTimeOut) if the wave ignored the request for 3 s (it still holds a CU
+ * until its 2-s lifetime ends; batch entries still run, one workgroup starting late). */
 ENET_CRC_API int enet_crc_ctx_stop_server(enet_crc_ctx* ctx);
 
 /*

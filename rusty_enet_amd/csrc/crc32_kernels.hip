@@ -44,9 +44,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "crc32_geometry.hpp"
 #include "crc32_kernels.hpp"
@@ -66,42 +68,52 @@ hipError_t set_device_kick_word(uint32_t* d_word) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_kick_word), &d_word, sizeof(d_word));
 }
 
-// The device's failure word (device address of a mapped, coherent pinned host word): a
-// batch kernel that gives up on an inter-wave wait writes its kFault* bit here, so the
-// host sees it without a copy (enet_crc_device_status).  Set before the first launch of
-// the ragged jobs kernel on the device (device_fault_word below).
-__device__ uint32_t* g_fault_word = nullptr;
+// Failure words (crc32_kernels.hpp: FaultWord): mapped, coherent pinned host memory that a
+// ragged jobs launch writes its kFault* bit into, so the host sees it without a copy.  Every
+// launch carries the device address of its word (RaggedJobsBatch::fault): a slot of a
+// synchronous entry passes its own, the asynchronous entries the device-wide one.
+hipError_t alloc_fault_word(FaultWord* w) {
+  *w = FaultWord{};
+  uint32_t* h = nullptr;
+  uint32_t* d = nullptr;
+  hipError_t e = hipHostMalloc((void**)&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) {
+    memset(h, 0, 64);
+    e = hipHostGetDevicePointer((void**)&d, h, 0);
+  }
+  if (e != hipSuccess) {
+    if (h) (void)hipHostFree(h);
+    return e;
+  }
+  w->host = h;
+  w->dev = d;
+  return hipSuccess;
+}
+
+void free_fault_word(FaultWord& w) {
+  if (w.host) (void)hipHostFree(const_cast<uint32_t*>(w.host));
+  w = FaultWord{};
+}
 
 namespace {
 constexpr int kMaxFaultDevices = 64;
 std::mutex g_fault_lock;
-uint32_t* g_fault_host[kMaxFaultDevices];  // host address of each device's word (never freed: 64 B)
+FaultWord g_fault_dev[kMaxFaultDevices];  // each device's word (never freed: 64 B)
 }  // namespace
 
-hipError_t device_fault_word(int dev, volatile uint32_t** host_word) {
+hipError_t device_fault_word(int dev, FaultWord* out) {
   if (dev < 0 || dev >= kMaxFaultDevices) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lk(g_fault_lock);
-  if (!g_fault_host[dev]) {
+  if (!g_fault_dev[dev].host) {
     int cur = -1;
     hipError_t e = hipGetDevice(&cur);
     if (e != hipSuccess) return e;
     if (cur != dev && (e = hipSetDevice(dev)) != hipSuccess) return e;
-    uint32_t* h = nullptr;
-    uint32_t* d = nullptr;
-    e = hipHostMalloc((void**)&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
-    if (e == hipSuccess) {
-      memset(h, 0, 64);
-      e = hipHostGetDevicePointer((void**)&d, h, 0);
-    }
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_fault_word), &d, sizeof(d));
+    e = alloc_fault_word(&g_fault_dev[dev]);
     if (cur != dev) (void)hipSetDevice(cur);
-    if (e != hipSuccess) {
-      if (h) (void)hipHostFree(h);
-      return e;
-    }
-    g_fault_host[dev] = h;
+    if (e != hipSuccess) return e;
   }
-  *host_word = g_fault_host[dev];
+  *out = g_fault_dev[dev];
   return hipSuccess;
 }
 
@@ -185,6 +197,44 @@ __device__ __forceinline__ uint32_t head_k(uint32_t v) {
   return v == 0 ? kOpTables.head_k[0]
                 : (v == 1 ? kOpTables.head_k[1] : (v == 2 ? kOpTables.head_k[2] : kOpTables.head_k[3]));
 }
+
+#ifdef ENET_CRC_CLOCK_STAMPS
+// Measurement build only (make variant NAME=clock DEFS=-DENET_CRC_CLOCK_STAMPS;
+// scripts/exp_clock_series.py): the shader clock each launch of the whole-line and the
+// ragged jobs kernel ran at.  Every wave stores its (shader cycles, 100-MHz ticks) between
+// entry and exit into its own cell of the launch's row (the row is a kernel argument the
+// launcher counts on the host): plain stores, no atomics (a first version added every
+// wave's numbers into one word per launch; those same-address atomics at the end of each
+// launch made it 60-85 % slower).  Clock = sum cycles / sum ticks x 100 MHz over the row
+// (MI355X_MICROARCH.md "DVFS give-back" (6)).
+constexpr uint32_t kClockSlots = 512;
+constexpr uint32_t kClockWaves = 4096;  // 256 CUs x 16 waves
+__device__ unsigned long long g_clock_cells[kClockSlots][kClockWaves][2];
+std::atomic<uint32_t> g_clock_next{0};  // host: the next launch's row
+struct ClockStamp {
+  uint64_t t0, r0;
+  uint32_t row;
+  __device__ explicit ClockStamp(uint32_t launch_row) : row(launch_row) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  __device__ ~ClockStamp() {
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint32_t w = blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63u) != 0u || w >= kClockWaves || row >= kClockSlots) return;
+    g_clock_cells[row][w][0] = t1 - t0;
+    g_clock_cells[row][w][1] = r1 - r0;
+  }
+};
+#define ENET_CRC_CLOCK_STAMP(row) ClockStamp clock_stamp_(row)
+#define ENET_CRC_CLOCK_ROW uint32_t clock_row = 0;
+#else
+#define ENET_CRC_CLOCK_STAMP(row) (void)0
+#define ENET_CRC_CLOCK_ROW
+#endif
 
 __device__ __forceinline__ int32_t wave_max_over_groups(int32_t v) {
   int32_t m = __builtin_amdgcn_readlane(v, 0);
@@ -649,6 +699,7 @@ struct UniformBatch {
   // (address and output), so one launch covers a head and a tail around a whole-line run.
   uint64_t skip_at = ~0ull;
   uint64_t skip = 0;
+  ENET_CRC_CLOCK_ROW  // measurement build only
 };
 
 // ---------------------------------------------------------------------------------
@@ -1333,6 +1384,7 @@ typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4;
 
 template <int NSL>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
+  ENET_CRC_CLOCK_STAMP(u.clock_row);
   send_servers_home();
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
@@ -1687,8 +1739,13 @@ struct RaggedJobsBatch {
   uint64_t count;
   uint64_t njobs;
   uint32_t job_packets;  // packets per job (<= kJobPackets), chosen so every workgroup gets the same job count
+  uint32_t* fault;       // this launch's failure word (device address; launch_ragged: FaultWord)
+  ENET_CRC_CLOCK_ROW     // measurement build only
 #ifdef ENET_CRC_TEST_HOOKS
-  uint32_t fault_k;  // test build: workgroup 0's (fault_k - 1)-th job reports its records never ready (0: none)
+  // Test build: workgroup 0 gives up the fault_kind wait (kFaultReady / kFaultConsumed /
+  // kFaultFreed) of its (fault_k - 1)-th job (fault_k == 0: none).
+  uint32_t fault_kind;
+  uint32_t fault_k;
 #endif
 };
 
@@ -1745,17 +1802,17 @@ __device__ __forceinline__ uint32_t lds_wait_eq(uint32_t a, uint32_t want, uint3
 }
 
 // A wave gave up a wait: mark its workgroup failed (LDS) and write the failure bit into the
-// device's failure word in host memory (one vector store by lane 0, system scope, waited
+// launch's failure word in host memory (one vector store by lane 0, system scope, waited
 // for; a racing writer can only replace one non-zero bit by another).
-__device__ __forceinline__ void report_fault(uint32_t fail, uint32_t bit) {
+__device__ __forceinline__ void report_fault(uint32_t fail, uint32_t bit, uint32_t* w) {
   if ((threadIdx.x & 63u) != 0u) return;
   lds_st32(fail, bit);
-  uint32_t* const w = g_fault_word;
   if (!w) return;
   asm volatile("global_store_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : : "v"(w), "v"(bit) : "memory");
 }
 
 __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_jobs_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
+  ENET_CRC_CLOCK_STAMP(b.clock_row);
   send_servers_home();
   constexpr int kDmaRing = kRaggedRing;
   __shared__ __attribute__((aligned(16))) RaggedJobsLds S;
@@ -1899,7 +1956,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   const uint32_t fail_a = lds_addr(&S.failed);
   // A wait's outcome: true if the flag came; a wave's own time-out is reported.
   auto waited = [&](uint32_t w, uint32_t bit) -> bool {
-    if (w == kWaitGaveUp) report_fault(fail_a, bit);
+    if (w == kWaitGaveUp) report_fault(fail_a, bit, b.fault);
     return w == kWaitOk;
   };
   auto make_round = [&](uint32_t d) -> RaggedRound {
@@ -1915,7 +1972,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       if (rv) seen_ready = k + 1u;
     }
 #ifdef ENET_CRC_TEST_HOOKS
-    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k) rv = waited(kWaitGaveUp, kFaultReady);
+    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k && b.fault_kind == kFaultReady) rv = waited(kWaitGaveUp, kFaultReady);
 #endif
     if (rv) {
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
@@ -1942,6 +1999,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
     }
+#ifdef ENET_CRC_TEST_HOOKS
+    if (blockIdx.x == 0 && k0 >= (uint32_t)kJobSlots && k0 + 1u == b.fault_k && b.fault_kind == kFaultFreed)
+      (void)waited(kWaitGaveUp, kFaultFreed);
+#endif
     // The checksum store is not waited for on its own: the done counter's wait below covers
     // it (LDS operations complete in order).
     if (c.k == 0 && (meta & kMetaStore)) lds_st32_nowait(lds_addr(&S.job[slot0].res[id]), __builtin_bswap32(~reg));
@@ -2000,6 +2061,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
       build = kb < (uint32_t)kJobSlots ||
               waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
+#ifdef ENET_CRC_TEST_HOOKS
+      if (blockIdx.x == 0 && kb >= (uint32_t)kJobSlots && kb + 1u == b.fault_k && b.fault_kind == kFaultConsumed)
+        build = waited(kWaitGaveUp, kFaultConsumed);
+#endif
       if (build) {
         if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
         job_dma(job_of(kb), bslot);
@@ -2148,7 +2213,11 @@ static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length, uint64_
 }
 
 template <int NSL>
-static hipError_t launch_uniform_lines(const UniformBatch& u, uint32_t* out, hipStream_t stream, unsigned blocks) {
+static hipError_t launch_uniform_lines(const UniformBatch& u0, uint32_t* out, hipStream_t stream, unsigned blocks) {
+  UniformBatch u = u0;
+#ifdef ENET_CRC_CLOCK_STAMPS
+  u.clock_row = g_clock_next.fetch_add(1);
+#endif
   hipLaunchKernelGGL((crc32_uniform_lines_kernel<NSL>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
@@ -2250,8 +2319,13 @@ hipError_t launch_single(const uint8_t* base, uint32_t length, uint32_t* out, hi
 // Below this many packets the sort costs more than the padding it saves.
 constexpr uint64_t kSortMinPackets = 4096;
 
+#ifdef ENET_CRC_TEST_HOOKS
+// Test build only: the shape of the last jobs-kernel launch (enet_crc_debug_ragged_shape).
+std::atomic<uint64_t> g_last_njobs{0}, g_last_job_packets{0}, g_last_grid{0};
+#endif
+
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
-                         uint64_t count, uint32_t* out, hipStream_t stream) {
+                         uint64_t count, uint32_t* out, hipStream_t stream, uint32_t* fault) {
   if (count == 0) return hipSuccess;
   hipError_t err;
   const unsigned blocks = grid_for(count, err);
@@ -2288,22 +2362,90 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     Launcher<true> L{b, out, stream, blocks};
     return L.streaming();
   }
-  // The kernel's failure channel must exist before its first launch on this device.
-  int dev = 0;
-  volatile uint32_t* fault = nullptr;
-  if ((err = hipGetDevice(&dev)) != hipSuccess || (err = device_fault_word(dev, &fault)) != hipSuccess) return err;
-  RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp};
+  // Without a word of its own the launch reports into the device's (asynchronous entries).
+  if (!fault) {
+    int dev = 0;
+    FaultWord w;
+    if ((err = hipGetDevice(&dev)) != hipSuccess || (err = device_fault_word(dev, &w)) != hipSuccess) return err;
+    fault = w.dev;
+  }
+  RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp, fault};
 #ifdef ENET_CRC_TEST_HOOKS
-  // Test build only (tests/test_gpu_hooks.py): ENET_CRC_TEST_JOB_FAULT=k makes workgroup 0's
-  // (k-1)-th job report that its records never became ready.
-  const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT");
-  jb.fault_k = fk ? (uint32_t)atoi(fk) : 0u;
+  // Test build only (tests/test_gpu_hooks.py): ENET_CRC_TEST_JOB_FAULT=<kind>:<k> makes
+  // workgroup 0 give up its <kind> wait (ready, consumed, freed) for its (k-1)-th job; a
+  // bare number means ready.
+  jb.fault_kind = 0;
+  jb.fault_k = 0;
+  if (const char* fk = getenv("ENET_CRC_TEST_JOB_FAULT")) {
+    const char* colon = strchr(fk, ':');
+    jb.fault_kind = kFaultReady;
+    if (colon) {
+      const size_t n = (size_t)(colon - fk);
+      jb.fault_kind = (n == 8 && !strncmp(fk, "consumed", 8)) ? kFaultConsumed
+                      : (n == 5 && !strncmp(fk, "freed", 5)) ? kFaultFreed
+                                                             : kFaultReady;
+      fk = colon + 1;
+    }
+    jb.fault_k = (uint32_t)atoi(fk);
+  }
+  g_last_njobs = njobs;
+  g_last_job_packets = jp;
+  g_last_grid = jblocks;
+#endif
+#ifdef ENET_CRC_CLOCK_STAMPS
+  jb.clock_row = g_clock_next.fetch_add(1);
 #endif
   hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
   return hipGetLastError();
 }
 
 }  // namespace enet_crc
+
+#ifdef ENET_CRC_TEST_HOOKS
+// Test build only: {jobs, packets per job, workgroups} of the last ragged jobs launch.
+extern "C" __attribute__((visibility("default"))) void enet_crc_debug_ragged_shape(uint64_t* out) {
+  out[0] = enet_crc::g_last_njobs;
+  out[1] = enet_crc::g_last_job_packets;
+  out[2] = enet_crc::g_last_grid;
+}
+#endif
+
+#ifdef ENET_CRC_CLOCK_STAMPS
+// Measurement build only: out[2 i], out[2 i + 1] = launch row i's shader cycles and 100-MHz
+// ticks summed over its waves (i < n <= kClockSlots), *launches = rows handed out so far;
+// reset != 0 zeroes the rows and restarts the count.
+extern "C" __attribute__((visibility("default"))) int enet_crc_debug_clock_stamps(unsigned long long* out, int n,
+                                                                                  unsigned* launches, int reset) {
+  using enet_crc::kClockSlots;
+  using enet_crc::kClockWaves;
+  if (n < 0 || n > (int)kClockSlots) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  if (n > 0) {
+    std::vector<unsigned long long> rows((size_t)n * kClockWaves * 2);
+    if (hipMemcpyFromSymbol(rows.data(), HIP_SYMBOL(enet_crc::g_clock_cells), rows.size() * sizeof(rows[0])) !=
+        hipSuccess)
+      return -3;
+    for (int i = 0; i < n; ++i) {
+      unsigned long long c = 0, t = 0;
+      for (uint32_t w = 0; w < kClockWaves; ++w) {
+        c += rows[((size_t)i * kClockWaves + w) * 2];
+        t += rows[((size_t)i * kClockWaves + w) * 2 + 1];
+      }
+      out[2 * i] = c;
+      out[2 * i + 1] = t;
+    }
+  }
+  if (launches) *launches = enet_crc::g_clock_next.load();
+  if (reset) {
+    std::vector<unsigned long long> zero((size_t)kClockSlots * kClockWaves * 2, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_clock_cells), zero.data(), zero.size() * sizeof(zero[0])) !=
+        hipSuccess)
+      return -3;
+    enet_crc::g_clock_next = 0;
+  }
+  return 0;
+}
+#endif
 
 #ifdef ENET_CRC_ROUND_STAMPS
 // Measurement build only: g_round_stamps (see its definition); reset != 0 zeroes them.

@@ -83,16 +83,21 @@ int stream_device(hipStream_t s) {
   return hipStreamGetDevice(s, &d) == hipSuccess ? d : -1;
 }
 
-// The device-side failure channel (crc32_kernels.hpp: device_fault_word): ENET_CRC_E_DEVICE
-// if a batch kernel on `dev` gave up since the word was last cleared (the word is cleared).
-// The synchronous entries call it after their last wait.
-int take_device_fault(int dev) {
-  volatile uint32_t* w = nullptr;
-  const hipError_t e = device_fault_word(dev, &w);
-  if (e != hipSuccess) return fail_hip(e);
-  if (*w == 0u) return ENET_CRC_OK;
-  (void)__atomic_exchange_n(const_cast<uint32_t*>(w), 0u, __ATOMIC_ACQ_REL);
-  return ENET_CRC_E_DEVICE;
+// The device-side failure channel (crc32_kernels.hpp: FaultWord).  Every slot of a
+// synchronous entry (a host-path staging slot, a ring slot) owns a word that only its own
+// launches write: the entry clears it before its launches and reads it after its last wait,
+// so a failure is reported by the call whose batch failed and by no other.
+// The asynchronous *_device entries report into the device's word (enet_crc_device_status).
+int slot_fault_word(FaultWord& w) {
+  if (w.host) return ENET_CRC_OK;
+  const hipError_t e = alloc_fault_word(&w);
+  return e == hipSuccess ? ENET_CRC_OK : fail_hip(e);
+}
+void clear_fault(FaultWord& w) {
+  if (w.host) __atomic_store_n(const_cast<uint32_t*>(w.host), 0u, __ATOMIC_RELEASE);
+}
+bool faulted(const FaultWord& w) {
+  return w.host && __atomic_load_n(const_cast<const uint32_t*>(w.host), __ATOMIC_ACQUIRE) != 0u;
 }
 
 }  // namespace
@@ -228,6 +233,7 @@ struct StageSlot {
   Mirror<uint32_t> out;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
+  FaultWord fault;     // failure word of this slot's ragged launches
   uint64_t first = 0;  // packet range staged in this slot
   uint64_t n = 0;
   bool busy = false;
@@ -361,6 +367,7 @@ struct RingSlot {
   uint32_t* d_crcs = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
+  FaultWord fault;  // failure word of this slot's launches (cleared by submit, read by wait)
   bool busy = false;
 };
 
@@ -426,6 +433,10 @@ int ragged_host_shard(Lane& L, const uint8_t* base, const uint64_t* h_offsets, c
     }
   } guard{L};
   const int fault_at = injected_stage_fault();
+  for (auto& s : L.slot) {
+    ENET_TRY(slot_fault_word(s.fault));
+    clear_fault(s.fault);  // both slots are idle here (quiesced by any earlier exit)
+  }
 
   // Drain a slot: wait for its kernel + D2H, copy checksums out.
   auto drain = [&](StageSlot& s) -> int {
@@ -461,7 +472,7 @@ int ragged_host_shard(Lane& L, const uint8_t* base, const uint64_t* h_offsets, c
     ENET_HIP_TRY(hipMemcpyAsync(s.bytes.d, s.bytes.h, span, hipMemcpyHostToDevice, s.stream));
     ENET_HIP_TRY(hipMemcpyAsync(s.offsets.d, s.offsets.h, n * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream));
     ENET_HIP_TRY(hipMemcpyAsync(s.lengths.d, s.lengths.h, n * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream));
-    ENET_HIP_TRY(launch_ragged(s.bytes.d, s.offsets.d, s.lengths.d, n, s.out.d, s.stream));
+    ENET_HIP_TRY(launch_ragged(s.bytes.d, s.offsets.d, s.lengths.d, n, s.out.d, s.stream, s.fault.dev));
     ENET_HIP_TRY(hipMemcpyAsync(s.out.h, s.out.d, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
     ENET_HIP_TRY(hipEventRecord(s.done, s.stream));
     p = q;
@@ -469,7 +480,9 @@ int ragged_host_shard(Lane& L, const uint8_t* base, const uint64_t* h_offsets, c
   }
   for (auto& s : L.slot) ENET_TRY(drain(s));
   guard.armed = false;
-  return take_device_fault(L.device);
+  for (auto& s : L.slot)
+    if (faulted(s.fault)) return ENET_CRC_E_DEVICE;
+  return ENET_CRC_OK;
 }
 
 void destroy_lane(Lane& L) {
@@ -480,6 +493,7 @@ void destroy_lane(Lane& L) {
     s.release();
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
+    free_fault_word(s.fault);
     s.stream = nullptr;
     s.done = nullptr;
   }
@@ -523,11 +537,11 @@ int enet_crc_device_status(int device, int clear) {
   const hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n <= 0) return e == hipSuccess || e == hipErrorNoDevice ? ENET_CRC_E_NO_DEVICE : fail_hip(e);
   if (device < 0 || device >= n) return ENET_CRC_E_NO_DEVICE;
-  volatile uint32_t* w = nullptr;
+  FaultWord w;
   const hipError_t fe = device_fault_word(device, &w);
   if (fe != hipSuccess) return fail_hip(fe);
-  const uint32_t v = clear ? __atomic_exchange_n(const_cast<uint32_t*>(w), 0u, __ATOMIC_ACQ_REL)
-                           : __atomic_load_n(const_cast<uint32_t*>(w), __ATOMIC_ACQUIRE);
+  uint32_t* const h = const_cast<uint32_t*>(w.host);
+  const uint32_t v = clear ? __atomic_exchange_n(h, 0u, __ATOMIC_ACQ_REL) : __atomic_load_n(h, __ATOMIC_ACQUIRE);
   return (int)(v & 0x7FFFFFFFu);
 }
 
@@ -613,11 +627,13 @@ void stop_mailbox(PerCall& c) { (void)stop_mailbox_bounded(c, kServerStopLimit);
 }  // namespace
 
 // Batch entry points of a context stop its server wave first: a resident wave holds
-// one CU, and the batched kernels size their grids to every CU.
-static void stop_server_for_batch(enet_crc_ctx* ctx) {
-  if (!ctx->call.mb_launched) return;
+// one CU, and the batched kernels size their grids to every CU.  False when the wave did
+// not stop within kServerStopLimit (wedged): the batch still runs, its workgroup on that CU
+// starting once the wave ends (at its 2-s lifetime); enet_crc_ctx_stop_server reports it.
+static bool stop_server_for_batch(enet_crc_ctx* ctx) {
+  if (!ctx->call.mb_launched) return true;
   DeviceGuard g(ctx->lanes[0].device);
-  stop_mailbox(ctx->call);
+  return stop_mailbox_bounded(ctx->call, kServerStopLimit);
 }
 
 int enet_crc_ctx_set_percall_mode(enet_crc_ctx* ctx, int mode) {
@@ -642,8 +658,9 @@ int enet_crc_ctx_percall_mode(enet_crc_ctx* ctx) {
 int enet_crc_ctx_stop_server(enet_crc_ctx* ctx) {
   if (!ctx) return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
-  stop_server_for_batch(ctx);
-  return ENET_CRC_OK;
+  // A wave that ignores the stop request: say so instead of returning OK while
+  // it still holds a CU.
+  return stop_server_for_batch(ctx) ? ENET_CRC_OK : fail_hip(hipErrorLaunchTimeOut);
 }
 
 void enet_crc_ctx_destroy(enet_crc_ctx* ctx) {
@@ -921,7 +938,7 @@ int enet_crc32_ragged_host(enet_crc_ctx* ctx, const void* h_base, const uint64_t
   if (count == 0) return ENET_CRC_OK;
   if (!h_base || !h_offsets || !h_lengths || !h_out) return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
-  stop_server_for_batch(ctx);
+  (void)stop_server_for_batch(ctx);  // a wedged wave only delays one workgroup
   const uint8_t* base = static_cast<const uint8_t*>(h_base);
   const uint32_t nl = (uint32_t)std::min<uint64_t>(ctx->lanes.size(), count);
   if (nl <= 1) return ragged_host_shard(ctx->lanes[0], base, h_offsets, h_lengths, count, h_out);
@@ -944,6 +961,7 @@ static void ring_free_slot(RingSlot& s) {
   if (s.d_crcs) (void)hipFree(s.d_crcs);
   if (s.done) (void)hipEventDestroy(s.done);
   if (s.stream) (void)hipStreamDestroy(s.stream);
+  free_fault_word(s.fault);
   s = RingSlot{};
 }
 
@@ -975,6 +993,7 @@ int enet_crc_ring_create(int device, uint32_t nslots, uint64_t slot_bytes, uint3
     if (se == hipSuccess) se = hipMalloc((void**)&s.d_offsets, slot_packets * sizeof(uint64_t));
     if (se == hipSuccess) se = hipMalloc((void**)&s.d_lengths, slot_packets * sizeof(uint32_t));
     if (se == hipSuccess) se = hipMalloc((void**)&s.d_crcs, slot_packets * sizeof(uint32_t));
+    if (se == hipSuccess) se = alloc_fault_word(&s.fault);
     if (se != hipSuccess) {
       enet_crc_ring_destroy(r);
       return fail_hip(se);
@@ -1023,6 +1042,7 @@ int enet_crc_ring_submit(enet_crc_ring* r, uint32_t slot, uint64_t count) {
     span = std::max(span, o + l);
   }
   DeviceGuard g(r->device);
+  clear_fault(s.fault);  // the slot is idle (not busy): nothing of its own writes the word
   hipError_t e = hipSuccess;
   if (count) {
     if (span) e = hipMemcpyAsync(s.d_data, s.h_data, span, hipMemcpyHostToDevice, s.stream);
@@ -1030,7 +1050,7 @@ int enet_crc_ring_submit(enet_crc_ring* r, uint32_t slot, uint64_t count) {
       e = hipMemcpyAsync(s.d_offsets, s.h_offsets, count * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(s.d_lengths, s.h_lengths, count * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = launch_ragged(s.d_data, s.d_offsets, s.d_lengths, count, s.d_crcs, s.stream);
+    if (e == hipSuccess) e = launch_ragged(s.d_data, s.d_offsets, s.d_lengths, count, s.d_crcs, s.stream, s.fault.dev);
     if (e == hipSuccess)
       e = hipMemcpyAsync(s.h_crcs, s.d_crcs, count * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream);
   }
@@ -1057,7 +1077,8 @@ int enet_crc_ring_wait(enet_crc_ring* r, uint32_t slot) {
     std::lock_guard<std::mutex> lk(r->lock);
     s.busy = false;
   }
-  return e == hipSuccess ? take_device_fault(r->device) : fail_hip(e);
+  if (e != hipSuccess) return fail_hip(e);
+  return faulted(s.fault) ? ENET_CRC_E_DEVICE : ENET_CRC_OK;
 }
 
 }  // extern "C"
@@ -1236,7 +1257,7 @@ static int range_ragged_host(enet_crc_ctx* ctx, bool decompress, const void* h_i
   if (!h_in || !h_in_offsets || !h_in_lengths || !h_out || !h_out_offsets || !h_out_limits || !h_sizes)
     return ENET_CRC_E_INVALID;
   std::lock_guard<std::mutex> lk(ctx->lock);
-  stop_server_for_batch(ctx);
+  (void)stop_server_for_batch(ctx);  // a wedged wave only delays one workgroup
   return range_host(ctx, decompress, static_cast<const uint8_t*>(h_in), h_in_offsets, h_in_lengths, count,
                     static_cast<uint8_t*>(h_out), h_out_offsets, h_out_limits, h_sizes);
 }

@@ -16,3 +16,10 @@ for path in sys.argv[1:]:
             print(f"  {k:10s} kernel {p['kernel_ms'] * 1000:7.1f} us  frac {p['frac']:.4f}  "
                   f"ceiling {p.get('read_ceiling_gbs')}  frac_of_ceiling {p.get('frac_of_ceiling')}"
                   + (f"  (cold {cold * 1000:.1f} us)" if cold else ""))
+    v = line.get("verify_256")
+    if v:
+        print(f"  verify_256: host {v['host_us']} us + slot adjust {v['slot_adjust_us']} us, ring {v['ring_us']} us, "
+              f"protocol {v['protocol_verify_received_us']} us, cpu 1 core {v['cpu_1core_us']} us, "
+              f"crossover batch {v['crossover_batch']}")
+        for b, row in v["sweep"].items():
+            print(f"    batch {b:>6s}: host {row['host_us']:8.1f} us  cpu {row['cpu_1core_us']:8.1f} us")

@@ -45,11 +45,12 @@ assert _native.LIB_PATH.endswith("libenet_crc_amd_testhooks.so"), _native.LIB_PA
 """
 
 
-def run_hooked(body: str, **env) -> None:
+def run_hooked(body: str, helpers: str = "", **env) -> None:
     if not os.path.exists(HOOKS_LIB):
         pytest.fail(f"{HOOKS_LIB} is not built (make)")
     e = dict(os.environ, ENET_CRC_AMD_LIB=HOOKS_LIB, **env)
-    r = subprocess.run([sys.executable, "-c", PRELUDE + textwrap.dedent(body) + "\nprint('HOOKED-OK')\n"],
+    code = PRELUDE + textwrap.dedent(helpers) + textwrap.dedent(body) + "\nprint('HOOKED-OK')\n"
+    r = subprocess.run([sys.executable, "-c", code],
                        capture_output=True, text=True, env=e, timeout=240)
     assert r.returncode == 0 and "HOOKED-OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
@@ -152,6 +153,11 @@ def test_wedged_server_never_hangs_the_context(dev):
         except rea.CrcError as e:
             assert e.status == _native.ENET_CRC_E_HIP, e.status
         assert time.perf_counter() - t0 < 0.5, time.perf_counter() - t0
+        try:
+            ctx.stop_server()                    # ADVICE r4: not OK while the wave still runs
+            raise SystemExit("stop_server returned OK next to a wedged server")
+        except rea.CrcError as e:
+            assert e.status == _native.ENET_CRC_E_HIP, e.status
         ctx.set_percall_mode(_native.ENET_CRC_PERCALL_ZEROCOPY)
         assert ctx([b"abc"]) == _oracle.crc32([b"abc"])
         t0 = time.perf_counter()
@@ -208,6 +214,157 @@ def test_ragged_kernel_failure_is_reported(dev):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
         assert rea.device_status(0) == 0
         ctx.close()
+    """)
+
+
+# Shared by the failure-channel tests below (child-process code): workgroup 0's jobs of the
+# last ragged jobs launch, from its shape (test build: enet_crc_debug_ragged_shape).
+SHAPE = """
+import ctypes
+def wg0_jobs():
+    sh = (ctypes.c_uint64 * 3)()
+    f = _native.lib().enet_crc_debug_ragged_shape
+    f.restype = None
+    f(sh)
+    njobs, jp, grid = int(sh[0]), int(sh[1]), int(sh[2])
+    assert njobs > 0 and jp > 0 and grid > 0, (njobs, jp, grid)
+    return [(k, k * grid * jp, min((k * grid + 1) * jp, N)) for k in range((njobs + grid - 1) // grid)], grid, jp
+
+def check_wg0(got, want, jobs, first_bad):
+    # workgroup 0's jobs before first_bad: each wholly exact or wholly unwritten (a job is
+    # flushed all at once), at least one exact (the failure came after a flush); from
+    # first_bad on: nothing written
+    flushed = 0
+    for k, a, b in jobs:
+        g = got[a:b]
+        if k >= first_bad:
+            assert (g == 0xFFFFFFFF).all(), ("written after the failure", k)
+        elif (g == 0xFFFFFFFF).all():
+            pass
+        else:
+            assert np.array_equal(g, want[a:b]), ("flushed job not exact", k)
+            flushed += 1
+    assert flushed >= 1, "no job flushed before the failure"
+    return flushed
+"""
+
+KINDS = {"ready": 1, "consumed": 2, "freed": 4}
+
+
+@pytest.mark.parametrize("kind", ["ready", "consumed", "freed"])
+def test_ragged_failure_mid_batch(dev, kind):
+    """each of the jobs kernel's three give-up paths, on a job of workgroup
+    0 well after its first flushes (the job number derived from the launch's own shape): the
+    right status bit in the device word, the jobs flushed before the failure exact, nothing of
+    workgroup 0 written from the failed job on, every other workgroup exact, and the next
+    launch clean."""
+    run_hooked(helpers=SHAPE, body=f"""
+        import os
+        import torch
+        dev = torch.device("cuda:0")
+        N = 1 << 20
+        lengths = ragged_lengths(43, N, lo=64, hi=256)
+        offsets = packed_offsets(lengths)
+        data = splitmix64_bytes(44, int(lengths.sum()))
+        want = _oracle.crc32_ragged(data, offsets, lengths, threads=8)
+        d = torch.from_numpy(data).to(dev)
+        off = torch.from_numpy(offsets.astype(np.int64)).to(dev)
+        ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
+        out = torch.full((N,), -1, dtype=torch.int32, device=dev)
+        rea.crc32_batch(d, offsets=off, lengths=ln, out=out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+        jobs, grid, jp = wg0_jobs()
+        assert len(jobs) >= 9, len(jobs)      # the consumed / freed waits start at job 6
+        k = len(jobs) - 3                     # a late job: earlier ones are flushed by then
+        assert rea.device_status(0, clear=True) == 0
+        os.environ["ENET_CRC_TEST_JOB_FAULT"] = "{kind}:%d" % (k + 1)
+        out.fill_(-1)
+        rea.crc32_batch(d, offsets=off, lengths=ln, out=out)
+        torch.cuda.synchronize()
+        del os.environ["ENET_CRC_TEST_JOB_FAULT"]
+        st = rea.device_status(0, clear=True)
+        assert st == {KINDS[kind]}, st
+        got = out.cpu().numpy().view(np.uint32)
+        in_wg0 = np.zeros(N, dtype=bool)
+        for _, a, b in jobs:
+            in_wg0[a:b] = True
+        assert np.array_equal(got[~in_wg0], want[~in_wg0])   # every other workgroup
+        flushed = check_wg0(got, want, jobs, k)
+        print("flushed before the failure:", flushed, "of", k, "jobs")
+        out.fill_(-1)
+        rea.crc32_batch(d, offsets=off, lengths=ln, out=out)  # the next launch is clean
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+        assert rea.device_status(0) == 0
+    """)
+
+
+def test_host_path_failure_mid_batch(dev):
+    """enet_crc32_ragged_host returns ENET_CRC_E_DEVICE for a failure on
+    workgroup 0's last job (one staging chunk: the job number comes from that launch's shape),
+    writes nothing into the device word, and the next call is exact."""
+    run_hooked(helpers=SHAPE, body="""
+        import os
+        N = 200_000                           # one staging chunk (< 256K packets, < 64 MiB)
+        lengths = ragged_lengths(45, N, lo=64, hi=256)
+        offsets = packed_offsets(lengths)
+        data = splitmix64_bytes(46, int(lengths.sum()))
+        want = _oracle.crc32_ragged(data, offsets, lengths, threads=8)
+        ctx = rea.Context(0)
+        assert np.array_equal(ctx.crc32_ragged_host(data, offsets, lengths), want)
+        jobs, grid, jp = wg0_jobs()
+        assert len(jobs) >= 2, len(jobs)
+        assert rea.device_status(0, clear=True) == 0
+        os.environ["ENET_CRC_TEST_JOB_FAULT"] = "ready:%d" % len(jobs)
+        try:
+            ctx.crc32_ragged_host(data, offsets, lengths)
+            raise SystemExit("no E_DEVICE")
+        except rea.CrcError as e:
+            assert e.status == _native.ENET_CRC_E_DEVICE, e.status
+        del os.environ["ENET_CRC_TEST_JOB_FAULT"]
+        assert rea.device_status(0) == 0     # the host path has words of its own
+        assert np.array_equal(ctx.crc32_ragged_host(data, offsets, lengths), want)
+        ctx.close()
+    """)
+
+
+def test_ring_failure_belongs_to_its_slot(dev):
+    """two ring slots in flight, only the second one's launch fails.  Each slot
+    owns its failure word: waiting for the second returns ENET_CRC_E_DEVICE, waiting for the
+    first (after it, so a shared word would already have been taken) returns OK with exact
+    checksums, the device word stays clear, and the failed slot is clean on its next submit."""
+    run_hooked("""
+        import os
+        from rusty_enet_amd.ring import ReceiveRing
+        n = 20_000
+        with ReceiveRing(0, nslots=2, slot_bytes=32 << 20, slot_packets=n) as ring:
+            want = []
+            for i in range(2):
+                data, off, ln, _ = ring.slot(i)
+                lengths = ragged_lengths(50 + i, n, lo=64, hi=1392)
+                offsets = packed_offsets(lengths)
+                total = int(lengths.sum())
+                data[:total] = splitmix64_bytes(60 + i, total)
+                off[:n] = offsets
+                ln[:n] = lengths
+                want.append(_oracle.crc32_ragged(data[:total].copy(), offsets, lengths))
+            assert rea.device_status(0, clear=True) == 0
+            ring.submit(0, n)
+            os.environ["ENET_CRC_TEST_JOB_FAULT"] = "ready:1"
+            ring.submit(1, n)
+            del os.environ["ENET_CRC_TEST_JOB_FAULT"]
+            try:
+                ring.wait(1)
+                raise SystemExit("no E_DEVICE from the failed slot")
+            except rea.CrcError as e:
+                assert e.status == _native.ENET_CRC_E_DEVICE, e.status
+            ring.wait(0)                         # OK: the failure was not its own
+            assert np.array_equal(ring.slot(0)[3][:n], want[0])
+            assert rea.device_status(0) == 0
+            ring.submit(1, n)
+            ring.wait(1)
+            assert np.array_equal(ring.slot(1)[3][:n], want[1])
     """)
 
 

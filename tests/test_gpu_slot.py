@@ -211,3 +211,62 @@ def test_insert_outgoing_mirror(dev):
     crcs = protocol.insert_outgoing(grams, hl, vs)
     assert [bytes(g) for g in grams] == refs
     assert crcs == [int.from_bytes(r[h:h + 4], "little") for r, h in zip(refs, hl)]
+
+
+def test_receive_batch_of_256_every_path(dev):
+    """the reference's receive batch, at most 256 datagrams per
+    service() (src/c/protocol.rs:1655), of 64-1392 B.  A batch that small takes the
+    streaming kernel (below kSortMinPackets, crc32_kernels.hip launch_ragged), not the jobs
+    kernel.  Bit-exact through the device entry, the host entry, one pinned ring slot, the
+    batched verify and protocol.verify_received, against the oracle's verdicts."""
+    from _data import packed_offsets, ragged_lengths
+    from rusty_enet_amd.ring import ReceiveRing
+
+    n = 256
+    rng = np.random.default_rng(256)
+    lengths = ragged_lengths(2560, n, lo=64, hi=1392)
+    grams, hs, vs = [], [], []
+    for p in range(n):
+        peer = 4095 if p % 17 == 0 else int(rng.integers(0, 4095))
+        hlen = 4 if p % 3 == 0 else 2
+        raw = (0x8000 if hlen == 4 else 0) | peer
+        header = bytes([raw >> 8, raw & 0xFF]) + (b"\x12\x34" if hlen == 4 else b"")
+        v = 0 if peer == 4095 else int(rng.integers(0, 1 << 32, dtype=np.uint64))
+        g = oracle_insert(header, splitmix64_bytes(7000 + p, int(lengths[p]) - hlen - 4), v)
+        if p % 5 == 1:  # a flipped bit past the peer-id word (the flags stay as sent)
+            g[int(rng.integers(2, g.size))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        grams.append(g)
+        hs.append(hlen + 4)
+        vs.append(v)
+    hs, vs = np.array(hs, dtype=np.uint32), np.array(vs, dtype=np.uint32)
+    want_ok, want_crc = oracle_verify(grams, hs, vs)
+    assert 0 < int(want_ok.sum()) < n
+    buf, offs, lens = pack(grams)
+    assert np.array_equal(lens, lengths)
+    stored = _oracle.crc32_ragged(buf, offs, lens)  # checksums of the datagrams as received
+    # device entry (streaming kernel) and host entry
+    got = u32(rea.crc32_batch(to_dev(buf, dev), offsets=to_dev(offs.astype(np.int64), dev),
+                              lengths=to_dev(lens.astype(np.int32), dev)))
+    torch.cuda.synchronize()
+    assert np.array_equal(got, stored)
+    with rea.Context(0) as ctx:
+        assert np.array_equal(ctx.crc32_ragged_host(buf, offs, lens), stored)
+    # one pinned ring slot
+    with ReceiveRing(0, nslots=1, slot_bytes=int(lens.sum()) + 64, slot_packets=n) as ring:
+        data, off, ln, crcs = ring.slot(0)
+        data[:buf.size] = buf
+        off[:n], ln[:n] = offs, lens
+        ring.submit(0, n)
+        ring.wait(0)
+        assert np.array_equal(crcs[:n], stored)
+    # batched verify on the device: checksums with the slot := v, verdicts
+    d_buf = to_dev(buf, dev)
+    crc_t, ok_t = rea.verify_batch(d_buf, to_dev(offs.astype(np.int64), dev), to_dev(lens.astype(np.int32), dev),
+                                   to_dev((hs - 4).astype(np.int32), dev),
+                                   to_dev(vs.view(np.int32), dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(ok_t), want_ok) and np.array_equal(u32(crc_t), want_crc)
+    # the Python mirror of the receive loop, connect_id read per datagram
+    it = iter([int(v) for v, g in zip(vs, grams) if ((int(g[0]) << 8 | int(g[1])) & 0x0FFF) != 4095])
+    verdicts = protocol.verify_received([bytes(g) for g in grams], lambda pid: next(it))
+    assert verdicts == [bool(x) for x in want_ok]
