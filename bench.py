@@ -474,9 +474,12 @@ def verify_batch(dev, batch: int = 256, reps: int = 200) -> dict:
                    "bytes": int(ln.sum())}
     data, off, ln = sample(batch, 300 + batch)
     crcs = ctx.crc32_ragged_host(data, off, ln)
-    # the receive loop's slot correction (connect_id instead of the wire value), in C per datagram
-    slot_us = med(lambda: [adj(int(c), 0x11223344, 0x55667788, int(n) - 6) for c, n in zip(crcs, ln)], 20)
-    call_us = med(lambda: [adj(1, 2, 3, 4) for _ in range(batch)], 20)  # the ctypes call alone
+    # the receive loop's slot correction (connect_id instead of the wire value), one C call per
+    # datagram; the same loop with bytes_after_slot = 0 (no table steps) is the ctypes cost
+    real_args = [(int(c), 0x11223344, 0x55667788, int(n) - 6) for c, n in zip(crcs, ln)]
+    zero_args = [(int(c), 0x11223344, 0x55667788, 0) for c in crcs]
+    slot_us = med(lambda: [adj(*a) for a in real_args], 50)
+    call_us = med(lambda: [adj(*a) for a in zero_args], 50)
     with ReceiveRing(dev.index or 0, nslots=1, slot_bytes=batch * 1392, slot_packets=batch) as ring:
         r_data, r_off, r_ln, r_crc = ring.slot(0)
         r_data[:data.size] = data
@@ -512,7 +515,8 @@ def verify_batch(dev, batch: int = 256, reps: int = 200) -> dict:
             "sweep": {str(b): rows[b] for b in sorted(rows)},
             "sample": f"{batch} datagrams of U{{64..1392}} B (the reference's receive batch, src/c/protocol.rs:1655), "
                       f"median of {reps}; host: enet_crc32_ragged_host from pageable memory; slot_adjust: "
-                      f"{batch} enet_crc32_slot_adjust calls less the ctypes call cost; ring: one pinned ring slot "
+                      f"{batch} enet_crc32_slot_adjust calls less the same calls with 0 bytes after the slot "
+                      "(the ctypes cost); ring: one pinned ring slot "
                       "submit + wait; protocol: the Python mirror verify_received (header parse, one GPU pass, "
                       "per-datagram correction); cpu: the C restatement of src/crc32.rs over the same datagrams on "
                       "one core; crossover: smallest batch of the sweep where host_us < cpu_1core_us"}

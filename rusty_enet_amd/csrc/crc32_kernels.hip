@@ -728,6 +728,9 @@ struct UniformBatch {
 typedef __attribute__((address_space(3))) void LdsVoid;
 typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
+#ifndef ENET_CRC_RAGGED_PAIRS  // ragged jobs kernel: 256-B pair loads; 0: the round-4 loads (A/B builds)
+#define ENET_CRC_RAGGED_PAIRS 1
+#endif
 #ifndef ENET_CRC_RAGGED_RING
 #define ENET_CRC_RAGGED_RING 3  // A/B variants may build 4 (with ENET_CRC_JOB_SLOTS=4 for the LDS)
 #endif
@@ -1505,18 +1508,36 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
 // (round_from_record).  Trailing bytes as in the uniform DMA kernel: each packet runs to
 // the next 4-byte boundary with the bytes past its end masked, then finish_word.
 // ---------------------------------------------------------------------------------
+// The DMA plan of one round for this lane: the address of its 16 B in pair 0 for each of its
+// two DMA packets (the packet's end minus 128 NS, plus the lane's offset inside the 256-B
+// pieces), and for each the first pair whose chunk of this lane is real (reaches the
+// packet's top word and lies in the caller's buffer).  With t = the top word's byte offset
+// in the round's 128 NS-byte piece space minus the lane offset, the chunk of pair P is real
+// iff 256 P + 16 > t, i.e. P >= (t + 240) / 256.  An invalid or empty packet has t = 128 NS
+// minus the lane offset: never real.
+// (ENET_CRC_RAGGED_PAIRS builds only.)
+struct PairPlan {
+  uint64_t db0, db1;
+  int32_t p0, p1;  // first real pair of each DMA packet's chunk
+};
+
 struct RaggedRound {
   uint64_t cb;          // this lane's chunk address at slot 0
   int32_t ns;           // slots of the round (wave-uniform)
   int32_t top_slot;     // slot of this lane's top chunk (ns: packet has no whole word)
   uint32_t meta;        // round_meta(); the trailing-byte field holds z (bytes run past the end)
   uint32_t id;          // packet id (output index)
+#if !ENET_CRC_RAGGED_PAIRS
   uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
+#endif
   bool fast;            // wave-uniform: top slots in B .. B + 1 (any in ring-length rounds), no fallback, ns <= kRaggedFastMax
   bool live;            // jobs kernel: the round is inside the batch (wave-uniform)
   uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
   uint32_t job_rounds;  // jobs kernel: rounds of that job
   int32_t top_uniform;  // B: the first top slot of a fast round (0 unless ns == kRaggedRing)
+#if ENET_CRC_RAGGED_PAIRS
+  PairPlan plan;        // this lane's DMA plan for the round
+#endif
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
@@ -1524,6 +1545,9 @@ constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRin
 // Per-lane round state from the group's packet record (ragged_record's fields; an invalid
 // group -- past the batch, or a re-read record -- is an empty packet at base4).  Every
 // quantity is derived with 32-bit arithmetic from the precomputed geometry.
+// kMinSlots: the fewest slots a round runs (the ring's reach into the next round); kEven:
+// rounds run an even number of slots (the 256-B pair loads).
+template <int kMinSlots = kRaggedRing, bool kEven = false>
 __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t id,
                                                          const LaneConsts& c) {
   const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
@@ -1533,7 +1557,7 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
   RaggedRound rr;
   const int32_t max_steps = wave_max_over_groups(nsteps);
-  rr.ns = max(kRaggedRing, max_steps);
+  rr.ns = max(kMinSlots, kEven ? (max_steps + 1) & ~1 : max_steps);
   rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
   rr.top_slot = rr.ns - nsteps;
   // This lane's chunk at the top step, relative to top: chunk_offset(g, k, nsteps-1, top)
@@ -1548,7 +1572,9 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
   rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
             (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
+#if !ENET_CRC_RAGGED_PAIRS
   rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
+#endif
   rr.id = id;
   // Fast: every packet starts at the same slot (same step count), no fallback chunk,
   // and the lanes whose top chunk lies before their packet are exactly the ones the
@@ -1560,11 +1586,12 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   // slots were issued by the previous round with per-lane sources, every later slot lies
   // inside every packet, and each lane masks its own top chunk at its top slot.
   rr.top_uniform = rr.ns - max_steps;  // B
-  const int32_t lim = rr.ns == kRaggedRing ? kRaggedRing : rr.top_uniform + 1;
+  const int32_t lim = rr.ns == kMinSlots ? kMinSlots : rr.top_uniform + 1;
   rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot > lim) && !fallback && rr.ns <= kRaggedFastMax;
   return rr;
 }
 
+#if !ENET_CRC_RAGGED_PAIRS
 // Source of this lane's slot-s DMA in round rr (the zero chunk before its top).
 __device__ __forceinline__ uint64_t ragged_src(const RaggedRound& rr, int32_t s, uint64_t dummy) {
   const bool real = s > rr.top_slot || (s == rr.top_slot && (rr.meta & kMetaDirect));
@@ -1674,6 +1701,241 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
   }
 }
 
+#endif  // !ENET_CRC_RAGGED_PAIRS
+
+#if ENET_CRC_RAGGED_PAIRS
+// ---------------------------------------------------------------------------------
+// Ragged rounds with 256-B loads.  The arithmetic and the compute
+// slots are those of the rounds above (8 lanes x 8 packets, 128 B of each packet per compute
+// slot); only the loads change.  A round runs an even number NS >= 4 of compute slots, and
+// compute slots 2P, 2P + 1 of every packet -- one contiguous 256-B piece of it -- arrive
+// together in "pair slot" P: two LDS-DMA instructions of 4 packets x 256 B each (instead of
+// two instructions of 8 packets x 128 B, a slot apart): fewer packets and fewer partial
+// lines per instruction.  Lane L of instruction i loads 16 B of packet 4 i + (L >> 4): half
+// h = ((L >> 3) ^ (L >> 4)) & 1 of its piece (the halves of odd packets swapped, so that
+// each compute slot's ds_read_b128 reads 256 distinct bytes per 16-lane quarter: no bank
+// conflicts), chunk L & 7 of that half.  Compute lane 8 g + k then reads its chunk 7 - k of
+// half 0 (compute slot 2P) and of half 1 (2P + 1) of packet g at fixed LDS offsets.
+// Ring: 2 pair slots (4 KiB) per wave; consuming pair P, the DMAs of P + 1 and P + 2 are in
+// flight.  The DMA lane decides per 16-B chunk whether it is real (at or after its packet's
+// top word, not below the caller's buffer) or the zero chunk.
+// ---------------------------------------------------------------------------------
+constexpr int kPairRing = 2;                                    // pair slots per wave
+// Lane k == 0 clears the z bytes past its packet's end in the last word (z in meta).
+__device__ __forceinline__ uint32_t last_word_mask(uint32_t meta, uint32_t k) {
+  return k == 0 ? 0xFFFFFFFFu >> (8u * ((meta >> kMetaNTailShift) & 3u)) : 0xFFFFFFFFu;
+}
+constexpr uint32_t kPairBytes = 2048;                           // one pair slot of one wave
+constexpr uint32_t kPairStride = kWavesPerBlock * kPairBytes;   // bytes between ring positions
+constexpr int kPairMinSlots = 2 * kPairRing;                    // a round's first 2 pairs come from the round before
+
+
+// From the two DMA packets' records (an invalid position reads as ax = info = 0: an empty
+// packet, every chunk the zero chunk).  A packet whose top lies within 16 B of the caller's
+// base also must not read below base4: its threshold is raised to that (o >= base4 - db).
+__device__ __forceinline__ PairPlan pair_plan(uint64_t ax0, uint32_t info0, uint64_t ax1, uint32_t info1, int32_t ns,
+                                              uint32_t dma_off, bool near_round, const LaneConsts& c) {
+  // In pair units, so that no intermediate overflows (ns < 2^26 from u32 lengths):
+  // (t + 240) / 256 = d / 2 + (128 (d & 1) + pad + 240 - lane offset) / 256, d = ns - nsteps.
+  auto one = [&](uint64_t ax, uint32_t info, uint64_t& db) -> int32_t {
+    const uint64_t piece0 = (ax & kRecAddrMask) - (uint64_t)kBytesPerStep * (uint64_t)ns;
+    db = piece0 + dma_off;
+    const uint32_t nsteps = info & kRecStepsMask, pad = (info >> kRecPadShift) << 2;
+    const uint32_t d = (uint32_t)ns - nsteps;
+    int32_t first = (int32_t)((d >> 1) + ((128u * (d & 1u) + pad + 240u - dma_off) >> 8));
+    if (near_round && ((ax >> kRecNearBit) & 1u)) {  // o = 256 P + lane offset >= base4 - piece0
+      const int64_t x = (int64_t)(c.base4 - piece0) - (int64_t)dma_off;
+      const int64_t pb = x <= 0 ? 0 : (x + 255) >> 8;
+      first = max(first, (int32_t)min(pb, (int64_t)0x40000000));
+    }
+    return first;
+  };
+  PairPlan p;
+  p.p0 = one(ax0, info0, p.db0);
+  p.p1 = one(ax1, info1, p.db1);
+  return p;
+}
+
+// A pair round's per-lane state from its packet record and the round header (ns, B and
+// `fast` are wave-uniform, from the job build's per-round max / min step counts).
+__device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t id,
+                                                              const LaneConsts& c, int32_t ns, int32_t B, bool fast,
+                                                              bool near_round) {
+  const uint64_t a1 = ax & kRecAddrMask;
+  const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
+  const uint32_t pad = (info >> kRecPadShift) << 2;
+  const uint32_t v = (uint32_t)(ax >> kRecVShift) & 3u;
+  const uint32_t z = (uint32_t)(ax >> kRecZShift) & 3u;
+  RaggedRound rr;
+  rr.ns = ns;
+  rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(ns - 1);
+  rr.top_slot = ns - nsteps;
+  const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
+  const bool inside = nsteps > 0 && rel > -16;
+  bool fb = false;
+  if (near_round) {  // wave-uniform: only rounds holding a packet near the caller's base
+    if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
+      const uint64_t top = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
+      fb = top - c.base4 < (uint64_t)(-rel);
+    }
+  }
+  const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
+  rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
+            (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
+  rr.id = id;
+  rr.top_uniform = B;
+  rr.fast = fast;
+  return rr;
+}
+
+// Per-lane constants of the pair ring.
+struct PairRing {
+  LdsVoid* slot0;    // this wave's pair slot 0
+  uint32_t ring0;    // its LDS byte address
+  uint32_t rd_a;     // this lane's read offset, half 0 (compute slot 2P)
+  uint32_t dma_off;  // this lane's byte offset inside its DMA packets' 256-B pieces
+  uint32_t q;        // pair slot of the pair being consumed (wave-uniform, 0 / 1)
+  u32x4 nextv;       // landed data of the compute slot about to be consumed
+  // Both DMAs of pair P of a round with plan pl into pair slot `slot`; `checked`: some chunk
+  // of this pair may lie before its packet's top (or below the caller's buffer).
+  __device__ __forceinline__ void issue(const PairPlan& pl, int32_t P, uint32_t slot, bool checked,
+                                        const LaneConsts& c) {
+    const uint64_t o = 256u * (uint64_t)P;
+    uint64_t s0 = pl.db0 + o, s1 = pl.db1 + o;
+    if (checked) {
+      s0 = P >= pl.p0 ? s0 : c.dummy;
+      s1 = P >= pl.p1 ? s1 : c.dummy;
+    }
+    LdsChar* const dst = (LdsChar*)slot0 + slot * kPairStride;
+    __builtin_amdgcn_global_load_lds((const void*)s0, (LdsVoid*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 0);
+  }
+  __device__ __forceinline__ uint32_t addr_a(uint32_t slot) const { return ring0 + slot * kPairStride + rd_a; }
+  __device__ __forceinline__ uint32_t addr_b(uint32_t slot) const { return ring0 + slot * kPairStride + (rd_a ^ 128u); }
+};
+
+// Consume compute slot s of a round of ns slots (s even: half 0 of pair s / 2, in pair slot
+// R.q): read the next compute slot's data into R.nextv (fused with the lookups of this slot
+// when `look`) and, after a half-0 slot, refill the pair slot just emptied with pair
+// s / 2 + 2 (of this round, or pair s / 2 + 2 - ns / 2 of the next).
+// Waits: consuming pair P, the DMAs of P + 1 and P + 2 may be in flight (vmcnt(2)); DMAs
+// complete in issue order.
+template <bool kLook>
+__device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan& cur, const PairPlan& nxt,
+                                          PairRing& R, const LaneConsts& c, bool cur_checked, uint32_t& h0,
+                                          uint32_t& h1, uint32_t& h2, uint32_t& h3, uint32_t w0, uint32_t w1,
+                                          uint32_t w2, uint32_t w3) {
+  const bool half0 = (s & 1) == 0;
+  const uint32_t next_addr = half0 ? R.addr_b(R.q) : R.addr_a(R.q ^ 1u);
+  if constexpr (kLook) {
+    horner_step_and_read<2>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
+  } else {
+    R.nextv = read_landed_slot<2>(next_addr);
+  }
+  if (half0) {
+    const int32_t f = s / 2 + kPairRing, np = ns / 2;  // the pair that refills pair slot R.q
+    if (f < np)
+      R.issue(cur, f, R.q, cur_checked, c);
+    else
+      R.issue(nxt, f - np, R.q, true, c);
+  } else {
+    R.q ^= 1u;
+  }
+}
+
+// A fast round (tops of every packet in compute slots T .. T + 1, or T .. 3 when NS = 4; no
+// fallback): unrolled; the pairs it issues for itself (P >= 2) need no check.
+template <int NS, int T = 0>
+__device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
+                                                PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
+                                                uint32_t& h2, uint32_t& h3) {
+  static_assert(NS % 2 == 0 && NS >= kPairMinSlots, "pair rounds");
+  static_assert(T == 0 || T == 1 || NS == kPairMinSlots, "leading zero slots beyond 1 only in minimum rounds");
+  constexpr int kMaskEnd = NS == kPairMinSlots ? kPairMinSlots - 1 : T + 1;  // last slot a top can be in
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const u32x4 v = R.nextv;
+    if (s < T) {
+      pair_step<false>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, 0, 0, 0, 0);
+      issue_order_fence();
+      continue;
+    }
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    if (s == NS - 1) w3 &= last_word_mask(cur.meta, c.k);  // data only: before the injection in mask_top
+    if (s <= kMaskEnd) {
+      const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
+      if (__builtin_amdgcn_ballot_w64(mine)) {
+        if (mine) mask_top(cur.meta, w0, w1, w2, w3);
+      }
+    }
+    if (s == T) {
+      h0 = w0;  // first top slot: every stream is still zero (M32^32(0) = 0), no lookups
+      h1 = w1;
+      h2 = w2;
+      h3 = w3;
+      pair_step<false>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, 0, 0, 0, 0);
+    } else {
+      pair_step<true>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, w0, w1, w2, w3);
+    }
+    issue_order_fence();
+  }
+}
+
+template <int... T>
+__device__ __forceinline__ bool pair_round_short(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
+                                                 PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
+                                                 uint32_t& h2, uint32_t& h3, std::integer_sequence<int, T...>) {
+  return ((cur.top_uniform == T ? (pair_round_fast<kPairMinSlots, T>(cur, pc, pn, R, c, h0, h1, h2, h3), true)
+                                : false) ||
+          ...);
+}
+
+// Fast rounds of NS = 6, 8, ..., kRaggedFastMax slots, T = 0 or 1.
+template <int... I>
+__device__ __forceinline__ bool pair_round_dispatch(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
+                                                    PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
+                                                    uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
+  if (cur.ns == kPairMinSlots)
+    return pair_round_short(cur, pc, pn, R, c, h0, h1, h2, h3, std::make_integer_sequence<int, kPairMinSlots>{});
+  if (cur.top_uniform == 0)
+    return ((cur.ns == kPairMinSlots + 2 * (I + 1)
+                 ? (pair_round_fast<kPairMinSlots + 2 * (I + 1), 0>(cur, pc, pn, R, c, h0, h1, h2, h3), true)
+                 : false) ||
+            ...);
+  if (cur.top_uniform == 1)
+    return ((cur.ns == kPairMinSlots + 2 * (I + 1)
+                 ? (pair_round_fast<kPairMinSlots + 2 * (I + 1), 1>(cur, pc, pn, R, c, h0, h1, h2, h3), true)
+                 : false) ||
+            ...);
+  return false;
+}
+
+// Any round: per-lane top slot and fallback chunks, runtime slot count, every pair checked.
+__device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
+                                                   PairRing& R, const LaneConsts& c, const uint32_t* lds,
+                                                   uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
+  for (int32_t s = 0; s < cur.ns; ++s) {
+    const u32x4 v = R.nextv;
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    const bool top = s == cur.top_slot;
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
+      if (top && (cur.meta & kMetaFallback))
+        load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
+    }
+    if (s == cur.ns - 1) w3 &= last_word_mask(cur.meta, c.k);
+    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
+    }
+    h0 = horner_main(lds, h0, w0, c.lk);
+    h1 = horner_main(lds, h1, w1, c.lk);
+    h2 = horner_main(lds, h2, w2, c.lk);
+    h3 = horner_main(lds, h3, w3, c.lk);
+    pair_step<false>(s, cur.ns, pc, pn, R, c, true, h0, h1, h2, h3, 0, 0, 0, 0);
+    issue_order_fence();
+  }
+}
+#endif  // ENET_CRC_RAGGED_PAIRS
+
 // ---------------------------------------------------------------------------------
 // Ragged kernel with in-kernel job sort (the default ragged path; no pre-pass, no
 // record scratch in HBM).  The batch is cut into jobs of up to kJobPackets consecutive
@@ -1699,7 +1961,7 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
 constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
 constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
 #ifndef ENET_CRC_JOB_SLOTS
-#define ENET_CRC_JOB_SLOTS 6
+#define ENET_CRC_JOB_SLOTS (ENET_CRC_RAGGED_PAIRS ? 4 : 6)  // pairs: the 64-KiB ring leaves room for 4
 #endif
 constexpr int kJobSlots = ENET_CRC_JOB_SLOTS;                    // job slots in LDS
 constexpr int kJobAhead = 2;                                     // jobs built ahead of the one claimed
@@ -1718,10 +1980,21 @@ static_assert(kJobRecBytes == kJobPackets * 12, "staging: u64 offsets + u32 leng
 struct JobSlot {
   u32x4 rec[kJobRecBytes / 16];
   uint32_t res[kJobPackets];
+#if ENET_CRC_RAGGED_PAIRS
+  // Per round of the job, from the job build: the largest and the smallest step count of its
+  // valid packets, and bit 0 = one of them begins within 16 B of the caller's base (a top
+  // chunk may need the fallback).  The round's slot count and its body follow from these
+  // alone (no cross-lane reduction per round).
+  u32x4 hdr[kJobRounds];
+#endif
 };
 struct RaggedJobsLds {
   uint32_t tables[kLdsDwords];
+#if ENET_CRC_RAGGED_PAIRS
+  u32x4 ring[kPairRing][kWavesPerBlock][kPairBytes / 16];
+#else
   u32x4 ring[kRaggedRing][kWavesPerBlock][64];
+#endif
   JobSlot job[kJobSlots];
   uint32_t ready[kJobSlots];     // k + 1 once the workgroup's k-th job has its records here
   uint32_t consumed[kJobSlots];  // rounds of the slot's job whose records have been read
@@ -1778,6 +2051,11 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(
 __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
+#if ENET_CRC_RAGGED_PAIRS
+__device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
+  asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+#endif
 
 #ifdef ENET_CRC_ROUND_STAMPS
 // Measurement build only (make variant NAME=stamps DEFS=-DENET_CRC_ROUND_STAMPS): per-wave
@@ -1864,10 +2142,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
     const uint64_t p0 = J * JP;
     if (p0 + kJobPackets <= b.count) {
+#if ENET_CRC_RAGGED_PAIRS
+      // The lane's byte offset through an asm statement: hipcc would otherwise hoist the three
+      // per-lane addresses out of the round loop and spill them (a scratch reload, then
+      // vmcnt(0), at every job build).
+      uint32_t l16;
+      asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(l16) : "v"(lane));
+      const char* const ob = reinterpret_cast<const char*>(b.offsets + p0) + l16;
+      const char* const lb = reinterpret_cast<const char*>(b.lengths + p0) + l16;
+      __builtin_amdgcn_global_load_lds((const void*)ob, (LdsVoid*)st, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(ob + 1024), (LdsVoid*)(st + 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)lb, (LdsVoid*)(st + 2048), 16, 0, 0);
+#else
       __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 2 * lane), (LdsVoid*)st, 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 + 2 * lane), (LdsVoid*)(st + 1024), 16, 0,
                                        0);
       __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 4 * lane), (LdsVoid*)(st + 2048), 16, 0, 0);
+#endif
     } else {
       // Not unrolled: one address live at a time (unrolled, hipcc hoisted all twelve out
       // of the round loop and spilled them to scratch: 18 MB of scratch writes per G2 launch).
@@ -1894,6 +2185,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                              o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
     const uint32_t len[4] = {ln.x, ln.y, ln.z, ln.w};
     const uint32_t n = job_count(J);
+#if ENET_CRC_RAGGED_PAIRS
+    const uint32_t hdr = lds_addr(&S.job[slot].hdr[0]);
+    if (lane < (uint32_t)kJobRounds) {  // max 0, min ~0, flags 0; in order before the atomics below
+      asm volatile("ds_write_b128 %0, %1" : : "v"(hdr + 16u * lane), "v"(u32x4{0u, 0xFFFFFFFFu, 0u, 0u}) : "memory");
+    }
+#endif
     uint64_t ax[4];
     uint32_t info[4], cls[4], rank[4];
 #pragma unroll
@@ -1901,7 +2198,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const bool v = 4u * lane + i < n;
       const RaggedRecord rec = ragged_record(b.base + off[i], len[i], c.base4);
       ax[i] = v ? rec.ax | ((uint64_t)(4u * lane + i) << kJobLidShift) : 0ull;
+#if ENET_CRC_RAGGED_PAIRS
+      info[i] = v ? rec.info : 0u;  // an invalid position reads as an empty packet at address 0 (pair_plan)
+#else
       info[i] = rec.info;
+#endif
       cls[i] = v ? (rec.nsteps < kStepClasses - 1 ? rec.nsteps : kStepClasses - 1) : (uint32_t)kStepClasses;
       rank[i] = 0;
 #pragma unroll
@@ -1936,6 +2237,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const uint32_t r = st + (q >> 3) * kJobRoundBytes;
       lds_st64(r + 8u * (q & 7u), ax[i]);
       lds_st32(r + 64u + 4u * (q & 7u), info[i]);
+#if ENET_CRC_RAGGED_PAIRS
+      if (cls[i] < (uint32_t)kStepClasses) {  // a valid packet: the round header
+        const uint32_t h = hdr + 16u * (q >> 3), ns_i = info[i] & kRecStepsMask;
+        asm volatile("ds_max_u32 %0, %1\n\tds_min_u32 %0, %1 offset:4" : : "v"(h), "v"(ns_i) : "memory");
+        if ((ax[i] >> kRecNearBit) & 1u) lds_or_nowait(h + 8u, 1u);
+      }
+#endif
     }
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
   };
@@ -1954,6 +2262,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   // Jobs this wave has seen ready / flushed (a job's flags are polled once per wave).
   uint32_t seen_ready = 0, seen_freed = 0;
   const uint32_t fail_a = lds_addr(&S.failed);
+#if ENET_CRC_RAGGED_PAIRS
+  // This lane's offset inside the 256-B pieces of its DMA packets (PairRing).
+  const uint32_t dma_off = 128u * (((lane >> 3) ^ (lane >> 4)) & 1u) + 16u * (lane & 7u);
+#endif
   // A wait's outcome: true if the flag came; a wave's own time-out is reported.
   auto waited = [&](uint32_t w, uint32_t bit) -> bool {
     if (w == kWaitGaveUp) report_fault(fail_a, bit, b.fault);
@@ -1974,6 +2286,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #ifdef ENET_CRC_TEST_HOOKS
     if (rv && blockIdx.x == 0 && k + 1u == b.fault_k && b.fault_kind == kFaultReady) rv = waited(kWaitGaveUp, kFaultReady);
 #endif
+#if ENET_CRC_RAGGED_PAIRS
+    u32x4 axd = {0, 0, 0, 0};  // the records of this lane's DMA packets lane / 16 and lane / 16 + 4
+    uint64_t infod = 0;
+    u32x4 hd = {0, 0, 0, 0};   // the round header: max steps, min steps, near flag
+    if (rv) {
+      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
+      const uint32_t gd = lane >> 4;
+      asm volatile(  // one round trip
+          "ds_read_b64 %0, %5\n\tds_read_b32 %1, %6\n\t"
+          "ds_read2_b64 %2, %7 offset1:4\n\tds_read2_b32 %3, %8 offset1:4\n\t"
+          "ds_read_b128 %4, %9\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(ax), "=&v"(info), "=&v"(axd), "=&v"(infod), "=&v"(hd)
+          : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(r + 64u + 4u * gd),
+            "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
+          : "memory");
+      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
+    }
+    const int32_t mx = (int32_t)__builtin_amdgcn_readfirstlane(hd.x);
+    const uint32_t mn = __builtin_amdgcn_readfirstlane(hd.y);
+    const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
+    const int32_t ns = max(kPairMinSlots, (mx + 1) & ~1), B = ns - mx;
+    // fast: every valid packet's top slot ns - nsteps in B .. B + 1 (any in minimum rounds,
+    // empty packets included), no fallback chunk, an unrolled body for ns
+    // A round with positions past the batch (the batch's last round) is fast only when all its
+    // pairs come checked from the round before (ns = kPairMinSlots): an invalid position's
+    // record is ax = 0, and an unchecked pair would read at address 0 - 128 ns.
+    const int32_t lim = ns == kPairMinSlots ? kPairMinSlots : B + 1;
+    const bool partial = (d - k * RJ + 1u) * kPacketsPerWave > n;
+    const bool fast = !near_round && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)mn <= (int64_t)lim &&
+                      (!partial || ns == kPairMinSlots);
+    RaggedRound rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u),
+                                            (uint32_t)(ax >> kJobLidShift) & 255u, c, ns, B, fast, near_round);
+    const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
+    rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, near_round, c);
+#else
     if (rv) {
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
       asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"  // one round trip
@@ -1983,6 +2330,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
     }
     RaggedRound rr = round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
+#endif
     rr.live = live;
     rr.job_k = k;
     rr.job_rounds = (n + kPacketsPerWave - 1) / kPacketsPerWave;
@@ -2035,6 +2383,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   if (!round_valid(rnd0)) return;
   RaggedRound cur = make_round(rnd0);
   RaggedRound nxt = make_round(rnd1);
+#if ENET_CRC_RAGGED_PAIRS
+  PairRing R;
+  R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
+  R.ring0 = lds_addr(&S.ring[0][wv][0]);
+  {
+    const uint32_t g = lane >> 3, k = lane & 7u, j = g & 3u;
+    R.rd_a = 1024u * (g >> 2) + 256u * j + 128u * (j & 1u) + 16u * (7u - k);
+    R.dma_off = dma_off;
+  }
+  R.q = 0;
+  R.issue(cur.plan, 0, 0, true, c);  // cur.ns >= kPairMinSlots: pairs 0 and 1
+  R.issue(cur.plan, 1, 1, true, c);
+  R.nextv = read_landed_slot<2>(R.addr_a(0));
+#else
   RaggedRing R;
   R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
   R.ring0 = lds_addr(&S.ring[0][wv][0]);
@@ -2043,6 +2405,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #pragma unroll
   for (int f = 0; f < kDmaRing; ++f) R.dma(ragged_src(cur, f, c.dummy));  // cur.ns >= kDmaRing
   R.nextv = read_landed_slot<kDmaRing - 1>(R.next_addr());
+#endif
 #ifdef ENET_CRC_ROUND_STAMPS
   uint64_t st_body = 0, st_build = 0, st_rounds = 0, st_comb = 0, st_make = 0;
   const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
@@ -2078,9 +2441,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // classes meeting in a round, fallback chunks, long packets) the generic loop.  Unrolled
     // bodies for the mixed rounds too made the kernel 143 KB instead of 59 KB and were no
     // faster; the generic loop alone is 6 % slower.
+#if ENET_CRC_RAGGED_PAIRS
+    if (!cur.fast || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
+                                          std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{}))
+      pair_round_generic(cur, cur.plan, nxt.plan, R, c, lds, h0, h1, h2, h3);
+#else
     if (!cur.fast || !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
                                             std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
       ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
+#endif
 #ifdef ENET_CRC_ROUND_STAMPS
     const uint64_t st_b1 = __builtin_amdgcn_s_memtime();
     st_body += st_b1 - st_b0;
@@ -2339,7 +2708,11 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
   // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
   // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
-  constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds, kMinJobRounds = kJobRounds / 2;
+#ifndef ENET_CRC_MAX_JOB_ROUNDS  // A/B builds: shorter jobs (a job's rounds run closer together in time)
+#define ENET_CRC_MAX_JOB_ROUNDS kJobRounds
+#endif
+  constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = ENET_CRC_MAX_JOB_ROUNDS,
+                     kMinJobRounds = kJobRounds / 2;
   const int cus = cu_count_for_current_device();
   if (cus <= 0) return hipErrorNoDevice;
   uint64_t jp = kMaxJobRounds * kRoundPackets, njobs = 0, best = ~0ull;

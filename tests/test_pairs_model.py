@@ -1,0 +1,177 @@
+"""Host model of the ragged jobs kernel's 256-B pair loads (ENET_CRC_RAGGED_PAIRS,
+crc32_kernels.hip: PairRing, pair_plan, pair_step).  Restates the kernel's index arithmetic
+and checks, for random rounds of 8 packets (empty, invalid, near-base and long packets, odd
+and even step counts):
+
+* every DMA source lies inside [base4, a1) of its packet's run, or is the zero chunk;
+* what compute lane 8 g + k reads at compute slot s from the LDS pair slot is exactly the
+  chunk the round's arithmetic expects there (the 16 bytes ending 16 (k + 8 i) bytes before
+  the packet's 4-byte-grid end, i = NS - 1 - s) when that chunk reaches the packet's top
+  word and lies in the caller's buffer, zeros otherwise (a top chunk below the buffer is the
+  compute lane's own fallback load, not the DMA's);
+* each 16-lane quarter of a compute slot's ds_read_b128 covers 256 distinct bytes of one
+  256-B bank row (no bank conflicts).
+"""
+import numpy as np
+
+LANES, G, STEP = 64, 8, 128
+MIN_SLOTS = 4
+
+
+def geometry(sa, length):
+    """ragged_record: (a1, nsteps, pad) of a packet run to the next 4-byte boundary."""
+    z = (4 - (sa + length) % 4) % 4 if length else 0
+    ea = sa + length + z
+    top, a1 = sa & ~3, ea & ~3
+    nwords = (a1 - top) >> 2
+    nsteps = ((nwords + 3) // 4 + G - 1) // G
+    return a1, nsteps, 128 * nsteps - 4 * nwords, top
+
+
+def round_slots(nsteps_list):
+    """The round header's max step count (valid packets only) -> NS."""
+    m = max(nsteps_list)
+    return max(MIN_SLOTS, (m + 1) & ~1)
+
+
+def lane_consts(lane):
+    g, k = lane >> 3, lane & 7
+    j = g & 3
+    rd_a = 1024 * (g >> 2) + 256 * j + 128 * (j & 1) + 16 * (7 - k)
+    jd = (lane >> 4) & 3
+    h = ((lane >> 3) & 1) ^ (jd & 1)
+    dma_off = 128 * h + 16 * (lane & 7)
+    return rd_a, dma_off
+
+
+def simulate_round(mem, base4, packets, valid, rng_dummy=None):
+    """packets: list of 8 (sa, length); valid: list of 8 bools.  Returns the LDS image of
+    every pair and the per-(lane, slot) data the compute lanes read."""
+    geo = [geometry(sa, ln) for sa, ln in packets]
+    nsteps = [gg[1] if v else 0 for gg, v in zip(geo, valid)]
+    ns = round_slots(nsteps)
+    # pair_plan per (lane, DMA packet): an invalid position's record reads as ax = info = 0
+    def plan(p, dma_off):
+        a1, nst, pad, top = geo[p]
+        if not valid[p]:
+            a1, nst, pad, near = 0, 0, 0, False
+        else:
+            near = top - base4 < 16
+        piece0 = a1 - STEP * ns
+        d = ns - nst
+        first = (d >> 1) + ((128 * (d & 1) + pad + 240 - dma_off) >> 8)
+        if near:
+            x = base4 - piece0 - dma_off
+            first = max(first, 0 if x <= 0 else (x + 255) >> 8)
+        return piece0 + dma_off, first
+
+    # The round header and the fast rule (make_round): fast rounds issue their own pairs P >= 2
+    # unchecked, straight from the plan; every such source must lie inside its packet.
+    vs = [n for n, v in zip(nsteps, valid) if v]
+    mx, mn = (max(vs), min(vs)) if vs else (0, 0xFFFFFFFF)
+    near_round = any(v and geo[p][3] - base4 < 16 for p, v in enumerate(valid))
+    B = ns - mx
+    lim = MIN_SLOTS if ns == MIN_SLOTS else B + 1
+    partial = not all(valid)
+    fast = (not near_round) and ns <= 14 and ns - mn <= lim and (not partial or ns == MIN_SLOTS)
+    if fast:
+        for P in range(2, ns // 2):
+            for i in range(2):
+                for L in range(LANES):
+                    gp = 4 * i + (L >> 4)
+                    dbo, _ = plan(gp, lane_consts(L)[1])
+                    src = dbo + 256 * P
+                    assert valid[gp] and base4 <= src and src + 16 <= geo[gp][0], ("unchecked", gp, P, L)
+    reads = {}
+    for P in range(ns // 2):
+        lds = np.full(2048, 0xEE, dtype=np.uint8)  # garbage unless written
+        for i in range(2):
+            for L in range(LANES):
+                gp = 4 * i + (L >> 4)
+                _, dma_off = lane_consts(L)
+                dbo, first = plan(gp, dma_off)
+                src = dbo + 256 * P
+                real = P >= first
+                if real:
+                    a1 = geo[gp][0]
+                    assert base4 <= src and src + 16 <= a1, (gp, P, L, src, a1)
+                    data = mem[src:src + 16]
+                else:
+                    data = np.zeros(16, dtype=np.uint8)
+                lds[1024 * i + 16 * L:1024 * i + 16 * L + 16] = data
+        for half in range(2):
+            s = 2 * P + half
+            addrs = []
+            for lane in range(LANES):
+                rd_a, _ = lane_consts(lane)
+                a = rd_a ^ (128 * half)
+                addrs.append(a)
+                reads[(lane, s)] = lds[a:a + 16].copy()
+            # bank check: each quarter reads 16 distinct 16-B bank groups of a 256-B row
+            for q in range(4):
+                banks = {(a % 256) // 16 for a in addrs[16 * q:16 * q + 16]}
+                assert len(banks) == 16, (P, half, q)
+    return ns, geo, reads
+
+
+def expected(mem, base4, packet, v, ns, lane, s):
+    (sa, ln) = packet
+    a1, nsteps, pad, top = geometry(sa, ln)
+    k = lane & 7
+    i = ns - 1 - s
+    A = a1 - 16 * (k + 8 * i + 1)
+    if not v or A + 16 <= top or A < base4:
+        return np.zeros(16, dtype=np.uint8)
+    return mem[A:A + 16]
+
+
+def check(seed, lengths_fn, trials=40):
+    rng = np.random.default_rng(seed)
+    for _ in range(trials):
+        lengths = lengths_fn(rng)
+        base = 64 + int(rng.integers(0, 4))  # the caller's buffer starts here
+        base4 = base & ~3
+        gaps = rng.integers(0, 3, size=8) * (rng.random(8) < 0.3)
+        sa, pk = base + int(rng.integers(0, 20)), []
+        for ln, gp in zip(lengths, gaps):
+            pk.append((sa, int(ln)))
+            sa += int(ln) + int(gp)
+        mem = rng.integers(0, 256, size=sa + 512, dtype=np.uint8)
+        valid = [bool(x) for x in rng.random(8) < 0.95]
+        if rng.random() < 0.3:  # the batch's last round: positions past the batch at its end
+            cut = int(rng.integers(1, 8))
+            valid = valid[:cut] + [False] * (8 - cut)
+        ns, geo, reads = simulate_round(mem, base4, pk, valid)
+        for lane in range(LANES):
+            g = lane >> 3
+            for s in range(ns):
+                want = expected(mem, base4, pk[g], valid[g], ns, lane, s)
+                got = reads[(lane, s)]
+                if not np.array_equal(got, want):
+                    # the only allowed difference: a fallback top chunk (below the buffer),
+                    # which the compute lane loads itself
+                    a1, nsteps, pad, top = geo[g]
+                    A = a1 - 16 * ((lane & 7) + 8 * (ns - 1 - s) + 1)
+                    assert valid[g] and A < base4 < A + 16 and A + 16 > top, (lane, s, A, base4)
+                    assert not got.any()
+
+
+def test_pair_loads_g2_lengths():
+    check(1, lambda r: r.integers(64, 1393, size=8))
+
+
+def test_pair_loads_class_sorted_rounds():
+    """Rounds as the job sort makes them: step counts within one or two of each other."""
+    def lens(r):
+        c = int(r.integers(1, 12))
+        return r.integers(max(1, 128 * (c - 1) - 60), 128 * c + 1, size=8)
+    check(2, lens)
+
+
+def test_pair_loads_short_empty_and_long():
+    check(3, lambda r: r.choice([0, 1, 2, 3, 5, 60, 64, 127, 128, 129, 511, 1392, 1396, 1791, 1792], size=8))
+
+
+def test_pair_loads_near_base():
+    """Packets starting within 16 B of the buffer base (the fallback top chunk)."""
+    check(4, lambda r: r.integers(1, 300, size=8), trials=80)
