@@ -848,6 +848,19 @@ def main(argv=None) -> int:
     ceil_fields = None if is_range else ceiling_fields(ceil, ceil_pre, spec[1] if ceil else None, nbytes,
                                                       nbytes / (kernel_ms / 1000.0) / 1e9)
 
+    # Cold: the same steps after an idle second, with only 5 launches of
+    # warmup and no read-ceiling pass before them: the chip starts high, drops its shader clock
+    # after a few ms of load and climbs back over ~30 ms (profiles/r05/clock);
+    # a bursty receive path sees this window.  Reported beside the line, never as its value.
+    cold = None
+    if not is_range and world == 1:
+        time.sleep(1.0)
+        for _ in range(5):
+            step()
+        wall_c, kms_c = time_steps(step, min(args.steps, 20), barrier, dev)
+        cold = {"kernel_ms": round(kms_c, 5), "frac": round(nbytes / (kms_c / 1000.0) / 1e9 / HBM_PEAK_GBS, 4),
+                "steps": min(args.steps, 20), "warmup": 5, "after_idle_s": 1.0}
+
     from rusty_enet_amd.shards import max_over_ranks
 
     wall_max, kernel_ms_max = max_over_ranks([wall, kernel_ms])
@@ -899,6 +912,8 @@ def main(argv=None) -> int:
         }
         if ceil_fields:
             line["roofline"].update(ceil_fields)
+        if cold:
+            line["roofline"]["cold"] = cold
         line.update(extra)
         line["devices"] = devices
         if is_range:

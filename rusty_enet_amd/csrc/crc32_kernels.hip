@@ -2455,8 +2455,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     st_body += st_b1 - st_b0;
     ++st_rounds;
 #endif
+#ifdef ENET_CRC_ABL_NOCOMBINE  // ablation build only (wrong checksums): the round end without its LDS trips
+    uint32_t reg = h0 ^ h1 ^ h2 ^ h3;
+#else
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
+#endif
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
 #ifdef ENET_CRC_ROUND_STAMPS
     reg = __builtin_amdgcn_readfirstlane(reg) == 0x12345678u ? reg + 1u : reg;  // the combine ends here

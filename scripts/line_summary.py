@@ -7,8 +7,10 @@ for path in sys.argv[1:]:
     with open(path) as f:
         line = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
     r = line["roofline"]
+    cold = r.get("cold")
     print(f"{path}: value {line['value']} GiB/s, kernel {r['kernel_ms'] * 1000:.1f} us, frac {r['frac']}, "
-          f"ceiling {r.get('read_ceiling_gbs')} GB/s, frac_of_ceiling {r.get('frac_of_ceiling')}")
+          f"ceiling {r.get('read_ceiling_gbs')} GB/s, frac_of_ceiling {r.get('frac_of_ceiling')}"
+          + (f"  (cold {cold['kernel_ms'] * 1000:.1f} us, frac {cold['frac']})" if cold else ""))
     for k in ("shard_2m", "mtu_1392", "ragged_g2", "large_64k", "frag_64k"):
         if k in line:
             p = line[k]
