@@ -1807,8 +1807,13 @@ struct PairRing {
       s1 = P >= pl.p1 ? s1 : c.dummy;
     }
     LdsChar* const dst = (LdsChar*)slot0 + slot * kPairStride;
+#ifdef ENET_CRC_ABL_NODMA  // ablation build only (wrong checksums): the ring is never loaded
+    if (s0 == 0 && s1 == 1) __builtin_trap();  // keeps the address arithmetic
+    (void)dst;
+#else
     __builtin_amdgcn_global_load_lds((const void*)s0, (LdsVoid*)dst, 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 0);
+#endif
   }
   __device__ __forceinline__ uint32_t addr_a(uint32_t slot) const { return ring0 + slot * kPairStride + rd_a; }
   __device__ __forceinline__ uint32_t addr_b(uint32_t slot) const { return ring0 + slot * kPairStride + (rd_a ^ 128u); }
@@ -1827,11 +1832,26 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
                                           uint32_t w2, uint32_t w3) {
   const bool half0 = (s & 1) == 0;
   const uint32_t next_addr = half0 ? R.addr_b(R.q) : R.addr_a(R.q ^ 1u);
+#ifdef ENET_CRC_ABL_NOWAIT  // ablation builds only (wrong checksums): no wait for the ring's DMAs
+  constexpr int kWait = 63;
+#else
+  constexpr int kWait = 2;
+#endif
+#ifdef ENET_CRC_ABL_NOLOOKUP  // ablation: the slot's data XORed into the streams, no table lookups
   if constexpr (kLook) {
-    horner_step_and_read<2>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
-  } else {
-    R.nextv = read_landed_slot<2>(next_addr);
+    h0 ^= w0;
+    h1 ^= w1;
+    h2 ^= w2;
+    h3 ^= w3;
   }
+  R.nextv = read_landed_slot<kWait>(next_addr);
+#else
+  if constexpr (kLook) {
+    horner_step_and_read<kWait>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
+  } else {
+    R.nextv = read_landed_slot<kWait>(next_addr);
+  }
+#endif
   if (half0) {
     const int32_t f = s / 2 + kPairRing, np = ns / 2;  // the pair that refills pair slot R.q
     if (f < np)
@@ -2177,7 +2197,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   // Phase B (>= kDmaRing DMAs after phase A): sort the job's packets by step class and
   // write its round records in place of the descriptors; then mark the slot ready.
   auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
+#ifdef ENET_CRC_ABL_NODMA  // no ring DMAs are issued after the descriptors' (the wait below counts on them)
+    asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+#else
     asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDmaRing - 1) : "memory");
+#endif
     const uint32_t st = lds_addr(&S.job[slot].rec[0]);
     const u32x4 o01 = lds_ld128(st + 32u * lane), o23 = lds_ld128(st + 32u * lane + 16u);
     const u32x4 ln = lds_ld128(st + 2048u + 16u * lane);
