@@ -731,6 +731,9 @@ constexpr int kUniformRing = 5;                              // LDS slots per wa
 #ifndef ENET_CRC_RAGGED_PAIRS  // ragged jobs kernel: 256-B pair loads; 0: the round-4 loads (A/B builds)
 #define ENET_CRC_RAGGED_PAIRS 1
 #endif
+#ifndef ENET_CRC_CLAIM_BATCH  // ragged jobs kernel: rounds claimed per LDS atomic (A/B builds: 2, 4)
+#define ENET_CRC_CLAIM_BATCH 1
+#endif
 #ifndef ENET_CRC_RAGGED_RING
 #define ENET_CRC_RAGGED_RING 3  // A/B variants may build 4 (with ENET_CRC_JOB_SLOTS=4 for the LDS)
 #endif
@@ -2434,10 +2437,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   uint64_t st_body = 0, st_build = 0, st_rounds = 0, st_comb = 0, st_make = 0;
   const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
 #endif
+#if ENET_CRC_CLAIM_BATCH > 1
+  // Rounds are claimed kClaimBatch at a time (one LDS atomic per batch instead of per round).
+  // A batch's rounds are consecutive and taken in order, so a round is still claimed before
+  // every later one of this wave, and the claimer of a job's first round still reaches it
+  // before any round of the job it builds.
+  constexpr uint32_t kClaimBatch = ENET_CRC_CLAIM_BATCH;
+  uint32_t claim_next = 0, claim_left = 0;
+#endif
   while (cur.live) {  // cur is round rnd0
+#if ENET_CRC_CLAIM_BATCH > 1
+    if (claim_left == 0) {
+      uint32_t t = 0;
+      if (lane == 0) t = lds_add_rtn(lds_addr(&S.next_dispatch), kClaimBatch);
+      claim_next = __builtin_amdgcn_readfirstlane(t);
+      claim_left = kClaimBatch;
+    }
+    const uint32_t d = claim_next;
+    ++claim_next;
+    --claim_left;
+#elif defined(ENET_CRC_CLAIM_STATIC)  // measurement build: round d = rnd1 + 16, no atomics
+    const uint32_t d = rnd1 + (uint32_t)kWavesPerBlock;
+#else
     uint32_t d = 0;
     if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
     d = __builtin_amdgcn_readfirstlane(d);
+#endif
     // Build duty: the claimer of a job's first round builds the job kJobAhead later (the
     // prologue built the first ones) once every round of the slot's previous job has read
     // its record.  That wait never closes a cycle: a round's record is read at the end of
