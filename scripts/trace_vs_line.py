@@ -5,8 +5,9 @@ durations against the bench line that process printed (tooling).
     python scripts/trace_vs_line.py gpurun_out/<tag>/trace_200_10 gpurun_out/<tag>/trace_200_10.json \
         [--csv profiles/r04/final/trace_200_10_kernel_trace.csv]
 
-The timed launches are the last `steps` launches of the headline kernel
-(crc32_uniform_lines_kernel<10>, G1) in the trace; their mean is compared with the line's
+The timed launches are launches 1 + warmup .. warmup + steps of the headline kernel
+(crc32_uniform_lines_kernel<10>, G1) in the trace (launch 0 is the verification step; since
+round 5 the line's cold window follows the timed steps); their mean is compared with the line's
 roofline.kernel_ms (HIP events around the same launches).  --csv writes the condensed
 per-launch series (launch, kernel, duration_us) of the whole process."""
 import argparse
@@ -45,9 +46,9 @@ def main() -> int:
     if line is None:
         print(f"no JSON line in {args.line}", file=sys.stderr)
         return 1
-    steps = int(line["steps"])
+    steps, warmup = int(line["steps"]), int(line["warmup"])
     head = [(e - s) / 1000.0 for s, e, k in rows if HEADLINE in k]
-    timed = head[-steps:]
+    timed = head[1 + warmup:1 + warmup + steps]
     mean = statistics.fmean(timed)
     line_us = float(line["roofline"]["kernel_ms"]) * 1000.0
     out = {"trace_dir": args.trace_dir, "headline_launches": len(head), "timed": len(timed),
