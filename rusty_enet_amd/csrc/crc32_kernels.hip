@@ -731,6 +731,9 @@ constexpr int kUniformRing = 5;                              // LDS slots per wa
 #ifndef ENET_CRC_RAGGED_PAIRS  // ragged jobs kernel: 256-B pair loads; 0: the round-4 loads (A/B builds)
 #define ENET_CRC_RAGGED_PAIRS 1
 #endif
+#ifndef ENET_CRC_MERGED_FLAGS  // jobs kernel: ready / freed flags read with the round's records (A/B)
+#define ENET_CRC_MERGED_FLAGS 0
+#endif
 #ifndef ENET_CRC_CLAIM_BATCH  // ragged jobs kernel: rounds claimed per LDS atomic (A/B builds: 2, 4)
 #define ENET_CRC_CLAIM_BATCH 1
 #endif
@@ -2091,7 +2094,36 @@ __device__ unsigned long long g_round_stamps[8];
 // is set: one wave that gives up makes every later wait of its workgroup return at once,
 // so a broken pipeline drains in one pass instead of one time-out per round.
 enum : uint32_t { kWaitOk = 0, kWaitGaveUp = 1, kWaitFailFast = 2 };
-__device__ __forceinline__ uint32_t lds_wait_eq(uint32_t a, uint32_t want, uint32_t fail) {
+#ifdef ENET_CRC_SPIN_STAMPS
+// Measurement build only (make variant NAME=spin DEFS=-DENET_CRC_SPIN_STAMPS;
+// scripts/exp_spin.py): per wave of the last ragged jobs launch, the loop's shader cycles and,
+// per wait kind (ready, consumed, freed), how many waits found their flag unset and the cycles
+// they spun.  Plain stores of per-wave cells at the wave's end, no atomics.
+constexpr uint32_t kSpinWaves = 4096;
+__device__ unsigned long long g_spin_cells[kSpinWaves][8];
+struct SpinAcc {
+  unsigned long long n = 0, cyc = 0;
+};
+#endif
+__device__ __forceinline__ uint32_t lds_wait_eq(uint32_t a, uint32_t want, uint32_t fail
+#ifdef ENET_CRC_SPIN_STAMPS
+                                                , SpinAcc* acc = nullptr
+#endif
+) {
+#ifdef ENET_CRC_SPIN_STAMPS
+  if (acc && __builtin_amdgcn_readfirstlane(lds_ld32(a)) != want) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    uint32_t r = kWaitGaveUp;
+    for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
+      if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) { r = kWaitOk; break; }
+      if (__builtin_amdgcn_readfirstlane(lds_ld32(fail)) != 0u) { r = kWaitFailFast; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    acc->n += 1;
+    acc->cyc += __builtin_amdgcn_s_memtime() - t0;
+    return r;
+  }
+#endif
   for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
     if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) return kWaitOk;
     if (__builtin_amdgcn_readfirstlane(lds_ld32(fail)) != 0u) return kWaitFailFast;
@@ -2286,6 +2318,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 
   // Jobs this wave has seen ready / flushed (a job's flags are polled once per wave).
   uint32_t seen_ready = 0, seen_freed = 0;
+#ifdef ENET_CRC_SPIN_STAMPS
+  SpinAcc spin_ready, spin_consumed, spin_freed;
+  uint64_t spin_rounds = 0;
+#define SPIN_ACC(a) , &a
+#else
+#define SPIN_ACC(a)
+#endif
   const uint32_t fail_a = lds_addr(&S.failed);
 #if ENET_CRC_RAGGED_PAIRS
   // This lane's offset inside the 256-B pieces of its DMA packets (PairRing).
@@ -2304,8 +2343,69 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint32_t n = J < b.njobs ? job_count(J) : 0u;
     const bool live = (d - k * RJ) * kPacketsPerWave < n;  // round_valid(d)
     bool rv = live;
+#if ENET_CRC_MERGED_FLAGS && ENET_CRC_RAGGED_PAIRS
+    u32x4 axd = {0, 0, 0, 0};  // the records of this lane's DMA packets lane / 16 and lane / 16 + 4
+    uint64_t infod = 0;
+    u32x4 hd = {0, 0, 0, 0};   // the round header: max steps, min steps, near flag
+    const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
+    const uint32_t gd = lane >> 4;
+    auto read_records = [&]() {
+      asm volatile(  // one round trip
+          "ds_read_b64 %0, %5\n\tds_read_b32 %1, %6\n\t"
+          "ds_read2_b64 %2, %7 offset1:4\n\tds_read2_b32 %3, %8 offset1:4\n\t"
+          "ds_read_b128 %4, %9\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(ax), "=&v"(info), "=&v"(axd), "=&v"(infod), "=&v"(hd)
+          : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(r + 64u + 4u * gd),
+            "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
+          : "memory");
+    };
+    // The job's ready flag and its slot's freed flag ride in the records' round trip: LDS
+    // operations are processed in order, so records read after a ready flag that reads set are
+    // the built ones (the builder stores them before the flag).  Only a flag that is not set
+    // yet costs a wait and a second read.
+    if (rv) {
+      uint32_t rdy, frd;
+      asm volatile(
+          "ds_read_b32 %5, %10\n\tds_read_b32 %6, %11\n\t"
+          "ds_read_b64 %0, %7\n\tds_read_b32 %1, %8\n\t"
+          "ds_read2_b64 %2, %9 offset1:4\n\tds_read2_b32 %3, %12 offset1:4\n\t"
+          "ds_read_b128 %4, %13\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(ax), "=&v"(info), "=&v"(axd), "=&v"(infod), "=&v"(hd), "=&v"(rdy), "=&v"(frd)
+          : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(lds_addr(&S.ready[slot])),
+            "v"(lds_addr(&S.freed[slot])), "v"(r + 64u + 4u * gd),
+            "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
+          : "memory");
+      if (k + 1u > seen_ready) {
+        if (__builtin_amdgcn_readfirstlane(rdy) == k + 1u) {
+          seen_ready = k + 1u;
+        } else {
+          rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a SPIN_ACC(spin_ready)), kFaultReady);
+          if (rv) {
+            seen_ready = k + 1u;
+            read_records();
+          }
+        }
+      }
+      // publish() of this job waits for the slot's previous job to be flushed: seen already?
+      if (k >= (uint32_t)kJobSlots && k + 1u - (uint32_t)kJobSlots > seen_freed &&
+          __builtin_amdgcn_readfirstlane(frd) == k + 1u - (uint32_t)kJobSlots)
+        seen_freed = k + 1u - (uint32_t)kJobSlots;
+    }
+#ifdef ENET_CRC_TEST_HOOKS
+    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k && b.fault_kind == kFaultReady) rv = waited(kWaitGaveUp, kFaultReady);
+#endif
+    if (rv) {
+      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
+    } else {
+      ax = 0;
+      info = 0;
+      axd = u32x4{0, 0, 0, 0};
+      infod = 0;
+      hd = u32x4{0, 0, 0, 0};
+    }
+#else
     if (rv && k + 1u > seen_ready) {
-      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
+      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a SPIN_ACC(spin_ready)), kFaultReady);
       if (rv) seen_ready = k + 1u;
     }
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2328,6 +2428,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
           : "memory");
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
     }
+#endif
+#endif
+#if ENET_CRC_RAGGED_PAIRS
     const int32_t mx = (int32_t)__builtin_amdgcn_readfirstlane(hd.x);
     const uint32_t mn = __builtin_amdgcn_readfirstlane(hd.y);
     const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
@@ -2369,7 +2472,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // writes the job's checksums to HBM.
     const uint32_t slot0 = k0 % kJobSlots;
     if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
-      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
+      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a SPIN_ACC(spin_freed)), kFaultFreed))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
     }
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2435,6 +2538,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   uint64_t st_body = 0, st_build = 0, st_rounds = 0, st_comb = 0, st_make = 0;
   const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef ENET_CRC_SPIN_STAMPS
+  const uint64_t spin_t0 = __builtin_amdgcn_s_memtime();
+#endif
 #if ENET_CRC_CLAIM_BATCH > 1
   // Rounds are claimed kClaimBatch at a time (one LDS atomic per batch instead of per round).
   // A batch's rounds are consecutive and taken in order, so a round is still claimed before
@@ -2470,7 +2576,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
     if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
       build = kb < (uint32_t)kJobSlots ||
-              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
+              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a SPIN_ACC(spin_consumed)), kFaultConsumed);
 #ifdef ENET_CRC_TEST_HOOKS
       if (blockIdx.x == 0 && kb >= (uint32_t)kJobSlots && kb + 1u == b.fault_k && b.fault_kind == kFaultConsumed)
         build = waited(kWaitGaveUp, kFaultConsumed);
@@ -2514,6 +2620,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     st_comb += __builtin_amdgcn_s_memtime() - st_b1;
 #endif
     publish(cur.job_k, cur.id, cur.meta, cur.job_rounds, reg);
+#ifdef ENET_CRC_ABL_EXTRA_TRIPS  // measurement build: n more dependent LDS round trips per round
+    {
+      uint32_t x = lds_addr(&S.failed);
+#pragma unroll
+      for (int t = 0; t < ENET_CRC_ABL_EXTRA_TRIPS; ++t) {
+        uint32_t v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(x) : "memory");
+        x += v;  // S.failed == 0: the same address, a true dependency
+      }
+    }
+#endif
+#ifdef ENET_CRC_ABL_EXTRA_IVALU  // measurement build: n more VALU instructions per round, 8 independent chains
+    {
+      uint32_t x0 = reg, x1 = reg + 1u, x2 = reg + 2u, x3 = reg + 3u, x4 = reg + 4u, x5 = reg + 5u, x6 = reg + 6u,
+               x7 = reg + 7u;
+#pragma unroll
+      for (int t = 0; t < ENET_CRC_ABL_EXTRA_IVALU / 8; ++t)
+        asm volatile(
+            "v_xad_u32 %0, %0, %0, %0\n\tv_xad_u32 %1, %1, %1, %1\n\tv_xad_u32 %2, %2, %2, %2\n\t"
+            "v_xad_u32 %3, %3, %3, %3\n\tv_xad_u32 %4, %4, %4, %4\n\tv_xad_u32 %5, %5, %5, %5\n\t"
+            "v_xad_u32 %6, %6, %6, %6\n\tv_xad_u32 %7, %7, %7, %7"
+            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7));
+      asm volatile("" : : "v"(x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7));
+    }
+#endif
+#ifdef ENET_CRC_ABL_EXTRA_SALU  // measurement build: n more SALU instructions per round, 4 independent chains
+    {
+      uint32_t y0 = rnd1, y1 = rnd1 + 1u, y2 = rnd1 + 2u, y3 = rnd1 + 3u;
+#pragma unroll
+      for (int t = 0; t < ENET_CRC_ABL_EXTRA_SALU / 4; ++t)
+        asm volatile("s_add_u32 %0, %0, 3\n\ts_add_u32 %1, %1, 5\n\ts_add_u32 %2, %2, 7\n\ts_add_u32 %3, %3, 9"
+                     : "+s"(y0), "+s"(y1), "+s"(y2), "+s"(y3) : : "scc");
+      asm volatile("" : : "s"(y0 ^ y1 ^ y2 ^ y3));
+    }
+#endif
+#ifdef ENET_CRC_ABL_EXTRA_VALU  // measurement build: n more dependent VALU instructions per round
+    {
+      uint32_t x = reg;
+#pragma unroll
+      for (int t = 0; t < ENET_CRC_ABL_EXTRA_VALU; ++t) asm volatile("v_xad_u32 %0, %0, %0, %0" : "+v"(x));
+      asm volatile("" : : "v"(x));
+    }
+#endif
 #ifdef ENET_CRC_ROUND_STAMPS
     const uint64_t st_j0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2532,7 +2681,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     rnd1 = d;
     cur = nxt;
     nxt = after;
+#ifdef ENET_CRC_SPIN_STAMPS
+    ++spin_rounds;
+#endif
   }
+#ifdef ENET_CRC_SPIN_STAMPS
+  {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint32_t w = blockIdx.x * kWavesPerBlock + wv;
+    if (lane == 0 && w < kSpinWaves) {
+      g_spin_cells[w][0] = t1 - spin_t0;
+      g_spin_cells[w][1] = spin_rounds;
+      g_spin_cells[w][2] = spin_ready.n;
+      g_spin_cells[w][3] = spin_ready.cyc;
+      g_spin_cells[w][4] = spin_consumed.n;
+      g_spin_cells[w][5] = spin_consumed.cyc;
+      g_spin_cells[w][6] = spin_freed.n;
+      g_spin_cells[w][7] = spin_freed.cyc;
+    }
+  }
+#endif
 #ifdef ENET_CRC_ROUND_STAMPS
   if (lane == 0) {
     atomicAdd(&g_round_stamps[0], (unsigned long long)st_body);
@@ -2866,6 +3034,28 @@ extern "C" __attribute__((visibility("default"))) int enet_crc_debug_clock_stamp
         hipSuccess)
       return -3;
     enet_crc::g_clock_next = 0;
+  }
+  return 0;
+}
+#endif
+
+#ifdef ENET_CRC_SPIN_STAMPS
+// Measurement build only: the per-wave cells of the last ragged jobs launch (8 words each, see
+// g_spin_cells), summed over the first `waves` waves into out[0..7]; reset != 0 zeroes them.
+extern "C" __attribute__((visibility("default"))) int enet_crc_debug_spin(unsigned long long* out, int waves, int reset) {
+  using enet_crc::kSpinWaves;
+  if (waves < 0 || waves > (int)kSpinWaves) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  std::vector<unsigned long long> cells((size_t)kSpinWaves * 8);
+  if (hipMemcpyFromSymbol(cells.data(), HIP_SYMBOL(enet_crc::g_spin_cells), cells.size() * sizeof(cells[0])) != hipSuccess)
+    return -3;
+  for (int j = 0; j < 8; ++j) out[j] = 0;
+  for (int w = 0; w < waves; ++w)
+    for (int j = 0; j < 8; ++j) out[j] += cells[(size_t)w * 8 + j];
+  if (reset) {
+    std::fill(cells.begin(), cells.end(), 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_spin_cells), cells.data(), cells.size() * sizeof(cells[0])) != hipSuccess)
+      return -3;
   }
   return 0;
 }
