@@ -378,6 +378,56 @@ __device__ __forceinline__ uint32_t combine_tree(const uint32_t* lds, uint32_t h
   return y;
 }
 
+#ifndef ENET_CRC_TREE_ASM  // jobs kernel: the tree levels as one asm statement (0: combine_tree, A/B builds)
+#define ENET_CRC_TREE_ASM 1
+#endif
+#if ENET_CRC_TREE_ASM
+// combine_tree's three tree levels for a kernel whose tables start at LDS address 0 (the
+// unreplicated tree sets at kTreeDword, byte 0x10000).  Each lookup address is ONE
+// v_lshlrev_b32_sdwa: byte j of y, times 4, written into the low half of `a`, whose high half
+// always holds 1 (dst_unused:UNUSED_PRESERVE), plus the set and table in the ds_read offset
+// (hipcc: v_bfe + v_lshl_or with the table base in a VGPR per table, 2 VALU per lookup).  The
+// levels' lane masks are set with scalar moves instead of hipcc's per-level saveexec of a
+// hoisted (and spilled to VGPR lanes) compare.  EXEC is all ones on entry (the round loop).
+// Lanes whose value does not move keep stale t; only lane k == 0's y is meaningful at the end.
+// Hazards (not inserted for inline asm): a VALU write then a DPP read of that VGPR needs 2
+// wait states (s_nop 1).
+#define ENET_TREE_LEVEL(MASK, OFF0, OFF1, OFF2, OFF3, SHL)                                                      \
+  "s_mov_b32 exec_lo, " MASK "\n\ts_mov_b32 exec_hi, " MASK "\n\t"                                             \
+  "v_lshlrev_b32_sdwa %[a], 2, %[y] dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_0\n\t" \
+  "ds_read_b32 %[t0], %[a] offset:" OFF0 "\n\t"                                                                 \
+  "v_lshlrev_b32_sdwa %[a], 2, %[y] dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_1\n\t" \
+  "ds_read_b32 %[t1], %[a] offset:" OFF1 "\n\t"                                                                 \
+  "v_lshlrev_b32_sdwa %[a], 2, %[y] dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_2\n\t" \
+  "ds_read_b32 %[t2], %[a] offset:" OFF2 "\n\t"                                                                 \
+  "v_lshlrev_b32_sdwa %[a], 2, %[y] dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_3\n\t" \
+  "ds_read_b32 %[t3], %[a] offset:" OFF3 "\n\t"                                                                 \
+  "s_waitcnt lgkmcnt(0)\n\t"                                                                                    \
+  "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                                                     \
+  "v_xor_b32 %[t0], %[t0], %[t3]\n\t"                                                                           \
+  "s_mov_b64 exec, %[sv]\n\t"                                                                                   \
+  "s_nop 1\n\t"                                                                                                 \
+  "v_xor_b32_dpp %[y], %[t0], %[y] row_shl:" SHL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+__device__ __forceinline__ uint32_t tree_levels_asm(uint32_t y, uint32_t& a) {
+  static_assert(kTreeDword * 4u == 0x10000u && kTreeLevels == 3, "the asm's addresses");
+  uint32_t t0, t1, t2, t3;
+  uint64_t sv;
+  asm volatile("s_mov_b64 %[sv], exec\n\t"
+               // M32^4: lanes k = 1, 3, 5, 7 of each group of 8, into k - 1
+               ENET_TREE_LEVEL("0xAAAAAAAA", "0", "1024", "2048", "3072", "1")
+               // M32^8: lanes k = 2, 6, into k - 2
+               ENET_TREE_LEVEL("0x44444444", "4096", "5120", "6144", "7168", "2")
+               // M32^16: lane k = 4, into k = 0
+               ENET_TREE_LEVEL("0x10101010", "8192", "9216", "10240", "11264", "4")
+               : [y] "+v"(y), [a] "+v"(a), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+                 [sv] "=&s"(sv)
+               :
+               : "memory");
+  return y;
+}
+#undef ENET_TREE_LEVEL
+#endif
+
 // combine_tree for the register-ring kernel's layout (kRegsLdsDwords): the first two tree
 // levels through the replicated tree block (conflict-free), the third unreplicated.
 __device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
@@ -730,6 +780,10 @@ typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
 #ifndef ENET_CRC_RAGGED_PAIRS  // ragged jobs kernel: 256-B pair loads; 0: the round-4 loads (A/B builds)
 #define ENET_CRC_RAGGED_PAIRS 1
+#endif
+#ifndef ENET_CRC_DIET  // jobs kernel: fewer instructions per round (top-chunk masks from an LDS table, the
+                       // checksum store and the last-word mask without lane compares); A/B builds
+#define ENET_CRC_DIET 1
 #endif
 #ifndef ENET_CRC_MERGED_FLAGS  // jobs kernel: ready / freed flags read with the round's records (A/B)
 #define ENET_CRC_MERGED_FLAGS 0
@@ -1727,8 +1781,59 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
 constexpr int kPairRing = 2;                                    // pair slots per wave
 // Lane k == 0 clears the z bytes past its packet's end in the last word (z in meta).
 __device__ __forceinline__ uint32_t last_word_mask(uint32_t meta, uint32_t k) {
+#if ENET_CRC_DIET
+  // No lane compare (hipcc hoists k == 0 into a lane mask, then spills it to a VGPR lane):
+  // kz = 0x18 on lane k == 0, else 0, by an arithmetic shift; the shift is 8 z there, else 0.
+  const uint32_t kz = 0x18u & (uint32_t)((int32_t)(k - 1u) >> 31);
+  return 0xFFFFFFFFu >> ((meta >> (kMetaNTailShift - 3)) & kz);
+#else
   return k == 0 ? 0xFFFFFFFFu >> (8u * ((meta >> kMetaNTailShift) & 3u)) : 0xFFFFFFFFu;
+#endif
 }
+
+#if ENET_CRC_DIET
+// Top-chunk masks from a 32-entry LDS table indexed by meta's head and v fields (5 bits):
+// entry e = {m0..m3}, {x0..x3} with w_i <- (w_i & m_i) ^ x_i (mask_top's words, the initial
+// register injected into the top word).  One asm statement: hipcc would put a plain LDS read
+// behind the in-flight ring DMAs (vmcnt(0)).
+struct TopMaskEntry {
+  u32x4 m, x;
+};
+__device__ __forceinline__ void fill_top_masks(TopMaskEntry* t) {
+  const uint32_t e = threadIdx.x;
+  if (e >= 32u) return;
+  const uint32_t head = e & kMetaHeadMask, v = (e >> kMetaVShift) & 3u;
+  uint32_t m[4] = {~0u, ~0u, ~0u, ~0u}, x[4] = {0u, 0u, 0u, 0u};
+  if (head >= 1u && head <= 4u) {
+    const uint32_t j0 = 4u - head;
+    for (uint32_t i = 0; i < 4; ++i) {
+      m[i] = i < j0 ? 0u : (i == j0 ? 0xFFFFFFFFu << (8u * v) : 0xFFFFFFFFu);
+      x[i] = i == j0 ? head_k(v) : 0u;
+    }
+  }
+  t[e].m = u32x4{m[0], m[1], m[2], m[3]};
+  t[e].x = u32x4{x[0], x[1], x[2], x[3]};
+}
+__device__ __forceinline__ void mask_top_lds(uint32_t meta, uint32_t table, uint32_t& w0, uint32_t& w1, uint32_t& w2,
+                                             uint32_t& w3) {
+  static_assert(kMetaHeadMask == 7 && kMetaVShift == 3, "the table index is meta & 0x1f");
+  u32x4 m, x;
+  uint32_t a;
+  asm volatile(
+      "v_bfe_u32 %2, %3, 0, 5\n\t"
+      "v_lshl_add_u32 %2, %2, 5, %4\n\t"
+      "ds_read_b128 %0, %2\n\t"
+      "ds_read_b128 %1, %2 offset:16\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(m), "=&v"(x), "=&v"(a)
+      : "v"(meta), "v"(table)
+      : "memory");
+  w0 = __builtin_amdgcn_bitop3_b32(w0, m.x, x.x, 0x6A);  // (w & m) ^ x
+  w1 = __builtin_amdgcn_bitop3_b32(w1, m.y, x.y, 0x6A);
+  w2 = __builtin_amdgcn_bitop3_b32(w2, m.z, x.z, 0x6A);
+  w3 = __builtin_amdgcn_bitop3_b32(w3, m.w, x.w, 0x6A);
+}
+#endif
 constexpr uint32_t kPairBytes = 2048;                           // one pair slot of one wave
 constexpr uint32_t kPairStride = kWavesPerBlock * kPairBytes;   // bytes between ring positions
 constexpr int kPairMinSlots = 2 * kPairRing;                    // a round's first 2 pairs come from the round before
@@ -1794,6 +1899,9 @@ __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint3
 
 // Per-lane constants of the pair ring.
 struct PairRing {
+#if ENET_CRC_DIET
+  uint32_t topmask;  // LDS address of the top-chunk mask table (mask_top_lds)
+#endif
   LdsVoid* slot0;    // this wave's pair slot 0
   uint32_t ring0;    // its LDS byte address
   uint32_t rd_a;     // this lane's read offset, half 0 (compute slot 2P)
@@ -1889,7 +1997,11 @@ __device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const Pa
     if (s <= kMaskEnd) {
       const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
       if (__builtin_amdgcn_ballot_w64(mine)) {
+#if ENET_CRC_DIET
+        if (mine) mask_top_lds(cur.meta, R.topmask, w0, w1, w2, w3);
+#else
         if (mine) mask_top(cur.meta, w0, w1, w2, w3);
+#endif
       }
     }
     if (s == T) {
@@ -1948,7 +2060,11 @@ __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const
     }
     if (s == cur.ns - 1) w3 &= last_word_mask(cur.meta, c.k);
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
+#if ENET_CRC_DIET
+      if (top && (cur.meta & kMetaHeadMask)) mask_top_lds(cur.meta, R.topmask, w0, w1, w2, w3);
+#else
       if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
+#endif
     }
     h0 = horner_main(lds, h0, w0, c.lk);
     h1 = horner_main(lds, h1, w1, c.lk);
@@ -2026,6 +2142,10 @@ struct RaggedJobsLds {
   uint32_t freed[kJobSlots];     // k + 1 once the k-th job's checksums are in HBM
   uint32_t next_dispatch;
   uint32_t failed;               // != 0 once a wave gave up a wait: later waits fail at once, nothing more is flushed
+#if ENET_CRC_DIET
+  TopMaskEntry topmask[32];      // mask_top_lds
+  uint32_t res_dummy[64];        // publish(): where the lanes that hold no checksum store theirs
+#endif
 };
 static_assert(sizeof(RaggedJobsLds) <= 160 * 1024, "LDS");
 
@@ -2159,6 +2279,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     S.next_dispatch = kWavesPerBlock * kLook;
     S.failed = 0;
   }
+#if ENET_CRC_DIET
+  fill_top_masks(S.topmask);
+#endif
   fill_lds(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
@@ -2186,6 +2309,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint64_t J = job_of(k);
     return J < b.njobs && (uint64_t)(d - k * RJ) * kPacketsPerWave < job_count(J);
   };
+#if ENET_CRC_DIET
+  // This workgroup's jobs k = 0 .. wg_jobs - 1 (job J = blockIdx.x + k grid); only its last can
+  // hold fewer than JP packets.  Per round then: live = d < wg_rounds, and the job's packet and
+  // round counts by one scalar compare (no 64-bit job arithmetic per round).
+  const uint32_t wg_jobs = (uint32_t)((b.njobs - blockIdx.x + gridDim.x - 1) / gridDim.x);
+  const uint32_t last_n = job_count(job_of(wg_jobs - 1u));
+  const uint32_t last_rounds = (last_n + kPacketsPerWave - 1) / kPacketsPerWave;
+  const uint32_t wg_rounds = (wg_jobs - 1u) * RJ + last_rounds;
+#endif
 
   // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
   // u32 lengths at +2048): three 16-B DMAs per lane (kJobPackets descriptors from the
@@ -2339,9 +2471,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     uint64_t ax = 0;
     uint32_t info = 0;
     const uint32_t k = div_rj(d), slot = k % kJobSlots;
+#if ENET_CRC_DIET
+    const bool live = d < wg_rounds;  // round_valid(d)
+    const uint32_t n = k + 1u == wg_jobs ? last_n : JP;
+#else
     const uint64_t J = job_of(k);
     const uint32_t n = J < b.njobs ? job_count(J) : 0u;
     const bool live = (d - k * RJ) * kPacketsPerWave < n;  // round_valid(d)
+#endif
     bool rv = live;
 #if ENET_CRC_MERGED_FLAGS && ENET_CRC_RAGGED_PAIRS
     u32x4 axd = {0, 0, 0, 0};  // the records of this lane's DMA packets lane / 16 and lane / 16 + 4
@@ -2461,7 +2598,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
     rr.live = live;
     rr.job_k = k;
+#if ENET_CRC_DIET
+    rr.job_rounds = k + 1u == wg_jobs ? last_rounds : RJ;
+#else
     rr.job_rounds = (n + kPacketsPerWave - 1) / kPacketsPerWave;
+#endif
     return rr;
   };
 
@@ -2481,7 +2622,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
     // The checksum store is not waited for on its own: the done counter's wait below covers
     // it (LDS operations complete in order).
+#if ENET_CRC_DIET
+    {  // every lane stores: lane k == 0 of a valid packet into res[id], the others into res_dummy
+      const uint32_t sel = (uint32_t)((int32_t)(meta << (31 - 10)) >> 31) &  // kMetaStore (bit 10)
+                           (uint32_t)((int32_t)(c.k - 1u) >> 31);            // k == 0
+      const uint32_t ra = lds_addr(&S.job[slot0].res[0]) + 4u * id, da = lds_addr(&S.res_dummy[0]) + 4u * lane;
+      lds_st32_nowait((sel & ra) | (~sel & da), __builtin_bswap32(~reg));
+    }
+#else
     if (c.k == 0 && (meta & kMetaStore)) lds_st32_nowait(lds_addr(&S.job[slot0].res[id]), __builtin_bswap32(~reg));
+#endif
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
     old = __builtin_amdgcn_readfirstlane(old);
@@ -2515,6 +2665,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   PairRing R;
   R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
   R.ring0 = lds_addr(&S.ring[0][wv][0]);
+#if ENET_CRC_DIET
+  R.topmask = lds_addr(&S.topmask[0]);
+#endif
   {
     const uint32_t g = lane >> 3, k = lane & 7u, j = g & 3u;
     R.rd_a = 1024u * (g >> 2) + 256u * j + 128u * (j & 1u) + 16u * (7u - k);
@@ -2540,6 +2693,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
 #ifdef ENET_CRC_SPIN_STAMPS
   const uint64_t spin_t0 = __builtin_amdgcn_s_memtime();
+#endif
+#if ENET_CRC_TREE_ASM
+  uint32_t tree_a = 0x10000u;  // tree_levels_asm's address register (high half 1, kept)
 #endif
 #if ENET_CRC_CLAIM_BATCH > 1
   // Rounds are claimed kClaimBatch at a time (one LDS atomic per batch instead of per round).
@@ -2574,7 +2730,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // checksum slot below waits only for an older job's flush).
     bool build = false;
     const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
+#if ENET_CRC_DIET
+    if (d == kd * RJ && kb >= first_jobs && kb < wg_jobs) {
+#else
     if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
+#endif
       build = kb < (uint32_t)kJobSlots ||
               waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a SPIN_ACC(spin_consumed)), kFaultConsumed);
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2610,6 +2770,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
 #ifdef ENET_CRC_ABL_NOCOMBINE  // ablation build only (wrong checksums): the round end without its LDS trips
     uint32_t reg = h0 ^ h1 ^ h2 ^ h3;
+#elif ENET_CRC_TREE_ASM
+    uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams
+    y = apply_rep(lds, y, h2, c.lk.lp1, c.lk);
+    y = apply_rep(lds, y, h3, c.lk.lp1, c.lk);
+    y = tree_levels_asm(y, tree_a);
+    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
 #else
     const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
