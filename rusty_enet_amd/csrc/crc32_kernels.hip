@@ -785,6 +785,10 @@ constexpr int kUniformRing = 5;                              // LDS slots per wa
                        // checksum store and the last-word mask without lane compares); A/B builds
 #define ENET_CRC_DIET 1
 #endif
+#ifndef ENET_CRC_HDR_PACKED  // jobs kernel: the job build packs each round's slot count, first top and
+                             // fast flag into its header (A/B builds)
+#define ENET_CRC_HDR_PACKED 1
+#endif
 #ifndef ENET_CRC_MERGED_FLAGS  // jobs kernel: ready / freed flags read with the round's records (A/B)
 #define ENET_CRC_MERGED_FLAGS 0
 #endif
@@ -2434,6 +2438,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       }
 #endif
     }
+#if ENET_CRC_RAGGED_PAIRS && ENET_CRC_HDR_PACKED
+    // Per round, make_round's rule evaluated once here: hdr.w = ns | B << 26 | fast << 31 (the
+    // header's max / min / near are complete: this wave's LDS atomics above are processed
+    // before its read below).
+    if (lane < RJ) {
+      const u32x4 hv = lds_ld128(hdr + 16u * lane);
+      const int32_t mx = (int32_t)hv.x;
+      const int32_t ns = max(kPairMinSlots, (mx + 1) & ~1), B = ns - mx;
+      const bool two_pairs = ns <= 2 * kPairRing;
+      const int32_t lim = two_pairs ? ns : B + 1;
+      const bool partial = (lane + 1u) * kPacketsPerWave > n;
+      const bool fast = hv.z == 0u && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)hv.y <= (int64_t)lim &&
+                        (!partial || two_pairs);
+      lds_st32(hdr + 16u * lane + 12u, (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u));
+    }
+#endif
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
   };
 
@@ -2568,6 +2588,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
 #endif
 #if ENET_CRC_RAGGED_PAIRS
+#if ENET_CRC_HDR_PACKED
+    const uint32_t hw = __builtin_amdgcn_readfirstlane(hd.w);  // ns | B << 26 | fast << 31 (job build)
+    const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
+    const int32_t ns = rv ? (int32_t)(hw & 0x3FFFFFFu) : kPairMinSlots, B = rv ? (int32_t)((hw >> 26) & 15u) : 0;
+    const bool fast = rv && (hw >> 31) != 0u;
+    (void)n;
+#else
     const int32_t mx = (int32_t)__builtin_amdgcn_readfirstlane(hd.x);
     const uint32_t mn = __builtin_amdgcn_readfirstlane(hd.y);
     const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
@@ -2581,6 +2608,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const bool partial = (d - k * RJ + 1u) * kPacketsPerWave > n;
     const bool fast = !near_round && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)mn <= (int64_t)lim &&
                       (!partial || ns == kPairMinSlots);
+#endif
     RaggedRound rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u),
                                             (uint32_t)(ax >> kJobLidShift) & 255u, c, ns, B, fast, near_round);
     const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
