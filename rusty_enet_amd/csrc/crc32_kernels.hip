@@ -789,6 +789,9 @@ constexpr int kUniformRing = 5;                              // LDS slots per wa
                              // fast flag into its header (A/B builds)
 #define ENET_CRC_HDR_PACKED 1
 #endif
+#ifndef ENET_CRC_NEAR_SPLIT  // jobs kernel: near-base rounds decoded by their own copy (A/B builds)
+#define ENET_CRC_NEAR_SPLIT 1
+#endif
 #ifndef ENET_CRC_MERGED_FLAGS  // jobs kernel: ready / freed flags read with the round's records (A/B)
 #define ENET_CRC_MERGED_FLAGS 0
 #endif
@@ -2609,10 +2612,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const bool fast = !near_round && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)mn <= (int64_t)lim &&
                       (!partial || ns == kPairMinSlots);
 #endif
+    const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
+#if ENET_CRC_NEAR_SPLIT
+    // Rounds holding a packet near the caller's base (the batch's first few) take their own copy
+    // of the decode: the others carry no near-base code at all (one scalar branch).
+    RaggedRound rr;
+    if (near_round) {
+      rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u,
+                                  c, ns, B, fast, true);
+      rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, true, c);
+    } else {
+      rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u,
+                                  c, ns, B, fast, false);
+      rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, false, c);
+    }
+#else
     RaggedRound rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u),
                                             (uint32_t)(ax >> kJobLidShift) & 255u, c, ns, B, fast, near_round);
-    const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
     rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, near_round, c);
+#endif
 #else
     if (rv) {
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
