@@ -175,3 +175,56 @@ def test_pair_loads_short_empty_and_long():
 def test_pair_loads_near_base():
     """Packets starting within 16 B of the buffer base (the fallback top chunk)."""
     check(4, lambda r: r.integers(1, 300, size=8), trials=80)
+
+
+def test_pair_ring_sequence():
+    """The pair ring across a wave's rounds (pair_step restated): every compute slot reads the
+    (round, pair, half) it consumes from the pair slot that pair was loaded into, no pair slot
+    is refilled before its last read, and each vmcnt(2) wait leaves only the DMAs of the most
+    recently issued pair in flight, never the one being read (DMAs complete in issue order)."""
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        rounds = [2 * int(x) for x in rng.integers(2, 8, size=int(rng.integers(1, 12)))] + [4]  # + a trailing round
+        slot_of = {}  # (round, pair) -> LDS pair slot
+        dmas = []     # issue order of (round, pair) (2 DMA instructions each)
+        reads_left = {}
+
+        def issue(r, P, q):
+            assert all(v == 0 for (rr, pp), v in reads_left.items() if slot_of.get((rr, pp)) == q), \
+                ("refilled before its last read", r, P, q)
+            assert P < rounds[r] // 2
+            slot_of[(r, P)] = q
+            reads_left[(r, P)] = 2
+            dmas.append((r, P))
+
+        def landed():  # after vmcnt(2): all but the last 2 DMA instructions (the last pair)
+            return dmas[:-1]
+
+        # prologue: pairs 0 and 1 of round 0 into pair slots 0 and 1, then read compute slot 0
+        issue(0, 0, 0)
+        issue(0, 1, 1)
+        assert (0, 0) in landed()
+        reads_left[(0, 0)] -= 1
+        nextv, q = (0, 0, 0), 0
+        for r in range(len(rounds) - 1):
+            ns = rounds[r]
+            for s in range(ns):
+                P, half = s >> 1, s & 1
+                assert nextv == (r, P, half), (nextv, r, P, half)
+                if half == 0:
+                    nxt = (r, P, 1)
+                    assert slot_of[(r, P)] == q
+                else:
+                    nxt = (r + 1, 0, 0) if s == ns - 1 else (r, P + 1, 0)
+                    assert slot_of[(nxt[0], nxt[1])] == q ^ 1, (nxt, q)
+                    assert (nxt[0], nxt[1]) in landed(), ("not landed at vmcnt(2)", nxt, dmas[-3:])
+                reads_left[(nxt[0], nxt[1])] -= 1
+                nextv = nxt
+                if half == 0:  # pair slot q's last half has been read: refill it with pair P + 2
+                    f = P + 2
+                    if f < ns // 2:
+                        issue(r, f, q)
+                    else:
+                        issue(r + 1, f - ns // 2, q)
+                else:
+                    q ^= 1
