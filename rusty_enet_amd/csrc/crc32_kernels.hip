@@ -792,6 +792,9 @@ constexpr int kUniformRing = 5;                              // LDS slots per wa
 #ifndef ENET_CRC_NEAR_SPLIT  // jobs kernel: near-base rounds decoded by their own copy (A/B builds)
 #define ENET_CRC_NEAR_SPLIT 1
 #endif
+#ifndef ENET_CRC_LANE0_ATOMICS  // jobs kernel: wave-level LDS counter updates without an EXEC change (A/B)
+#define ENET_CRC_LANE0_ATOMICS 0
+#endif
 #ifndef ENET_CRC_MERGED_FLAGS  // jobs kernel: ready / freed flags read with the round's records (A/B)
 #define ENET_CRC_MERGED_FLAGS 0
 #endif
@@ -2202,6 +2205,23 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(
 __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
+#if ENET_CRC_LANE0_ATOMICS
+// A counter update of the wave (lane 0's), issued by every lane: lane 0 adds v to the counter,
+// the others add 0 to their own word of a dummy row (64 distinct words: no conflicts, no
+// serialisation), so no lane compare and no EXEC change is needed.  l0 = all ones on lane 0
+// (a per-lane constant), drow = the lane's word of the dummy row.
+__device__ __forceinline__ uint32_t lds_add_rtn_l0(uint32_t a, uint32_t v, uint32_t l0, uint32_t drow) {
+  uint32_t old;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(old)
+               : "v"((l0 & a) | (~l0 & drow)), "v"(l0 & v)
+               : "memory");
+  return __builtin_amdgcn_readfirstlane(old);
+}
+__device__ __forceinline__ void lds_add_nowait_l0(uint32_t a, uint32_t v, uint32_t l0, uint32_t drow) {
+  asm volatile("ds_add_u32 %0, %1" : : "v"((l0 & a) | (~l0 & drow)), "v"(l0 & v) : "memory");
+}
+#endif
 #if ENET_CRC_RAGGED_PAIRS
 __device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
@@ -2295,6 +2315,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
+#if ENET_CRC_LANE0_ATOMICS
+  static_assert(ENET_CRC_DIET, "the dummy row is res_dummy");
+  const uint32_t l0 = (uint32_t)((int32_t)(lane - 1u) >> 31);  // all ones on lane 0
+  const uint32_t drow = lds_addr(&S.res_dummy[0]) + 4u * lane;
+#endif
 
   auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
   const uint32_t JP = b.job_packets;
@@ -2555,7 +2580,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     if (rv && blockIdx.x == 0 && k + 1u == b.fault_k && b.fault_kind == kFaultReady) rv = waited(kWaitGaveUp, kFaultReady);
 #endif
     if (rv) {
+#if ENET_CRC_LANE0_ATOMICS
+      lds_add_nowait_l0(lds_addr(&S.consumed[slot]), 1u, l0, drow);
+#else
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
+#endif
     } else {
       ax = 0;
       info = 0;
@@ -2586,7 +2615,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
           : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(r + 64u + 4u * gd),
             "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
           : "memory");
+#if ENET_CRC_LANE0_ATOMICS
+      lds_add_nowait_l0(lds_addr(&S.consumed[slot]), 1u, l0, drow);
+#else
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
+#endif
     }
 #endif
 #endif
@@ -2679,8 +2712,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     if (c.k == 0 && (meta & kMetaStore)) lds_st32_nowait(lds_addr(&S.job[slot0].res[id]), __builtin_bswap32(~reg));
 #endif
     uint32_t old = 0;
+#if ENET_CRC_LANE0_ATOMICS
+    old = lds_add_rtn_l0(lds_addr(&S.done[slot0]), 1u, l0, drow);
+#else
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
     old = __builtin_amdgcn_readfirstlane(old);
+#endif
     // After a failure in the workgroup nothing more is flushed: a job whose records or
     // result slot were skipped would leave stale checksums in res[].
     if (old + 1u == job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
@@ -2765,9 +2802,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #elif defined(ENET_CRC_CLAIM_STATIC)  // measurement build: round d = rnd1 + 16, no atomics
     const uint32_t d = rnd1 + (uint32_t)kWavesPerBlock;
 #else
+#if ENET_CRC_LANE0_ATOMICS
+    const uint32_t d = lds_add_rtn_l0(lds_addr(&S.next_dispatch), 1u, l0, drow);
+#else
     uint32_t d = 0;
     if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
     d = __builtin_amdgcn_readfirstlane(d);
+#endif
 #endif
     // Build duty: the claimer of a job's first round builds the job kJobAhead later (the
     // prologue built the first ones) once every round of the slot's previous job has read
