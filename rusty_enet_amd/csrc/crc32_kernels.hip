@@ -704,6 +704,16 @@ constexpr uint64_t kRecAddrMask = (1ull << 48) - 1;
 constexpr int kRecVShift = 48, kRecZShift = 50, kRecNearBit = 52, kRecValidBit = 53;
 constexpr uint32_t kRecStepsMask = (1u << 26) - 1;
 constexpr int kRecPadShift = 26;
+// Round-relative records (ENET_CRC_REC2: the job build's last pass, once the round's slot
+// count ns is known):
+//   ax   (u64): piece0 = a1 - 128 ns (48 bits) | valid << 48 | near << 49 | v << 51 |
+//               empty << 53 | z << 54 | local id << 56   (v, empty, z at their meta positions + 48)
+//   info (u32): d = ns - nsteps (the packet's top slot) | (pad / 4) << 26
+// A position past the job: ax = 0, info = ns.  Readers take d = ns (never real) whenever the
+// valid bit is clear -- also for the all-zero record of a round that is not live.  (Device and
+// host virtual addresses here are far above 128 ns <= 8 GiB, so piece0 never wraps.)
+constexpr int kRec2ValidBit = 48, kRec2NearBit = 49, kRec2LidShift = 56;
+constexpr uint32_t kRec2MetaBits = 0xF8u;  // (ax >> 48) & this = v | empty | z in meta layout
 
 struct RaggedRecord {
   uint64_t ax;
@@ -794,6 +804,9 @@ constexpr int kUniformRing = 5;                              // LDS slots per wa
 #endif
 #ifndef ENET_CRC_LANE0_ATOMICS  // jobs kernel: wave-level LDS counter updates without an EXEC change (A/B)
 #define ENET_CRC_LANE0_ATOMICS 0
+#endif
+#ifndef ENET_CRC_REC2  // jobs kernel: the job build rewrites each record relative to its round (A/B)
+#define ENET_CRC_REC2 0
 #endif
 #ifndef ENET_CRC_MERGED_FLAGS  // jobs kernel: ready / freed flags read with the round's records (A/B)
 #define ENET_CRC_MERGED_FLAGS 0
@@ -1875,6 +1888,31 @@ __device__ __forceinline__ PairPlan pair_plan(uint64_t ax0, uint32_t info0, uint
   return p;
 }
 
+#if ENET_CRC_REC2
+// pair_plan from round-relative records: piece0 and d come stored.  A record without the valid
+// bit (a position past the job, or the zeros of a round that is not live) is never real.
+__device__ __forceinline__ PairPlan pair_plan2(uint64_t ax0, uint32_t info0, uint64_t ax1, uint32_t info1, int32_t ns,
+                                               uint32_t dma_off, bool near_round, const LaneConsts& c) {
+  auto one = [&](uint64_t ax, uint32_t info, uint64_t& db) -> int32_t {
+    const uint64_t piece0 = ax & kRecAddrMask;
+    db = piece0 + dma_off;
+    const bool valid = (ax >> kRec2ValidBit) & 1u;
+    const uint32_t d = valid ? info & kRecStepsMask : (uint32_t)ns, pad = (info >> kRecPadShift) << 2;
+    int32_t first = (int32_t)((d >> 1) + ((128u * (d & 1u) + pad + 240u - dma_off) >> 8));
+    if (near_round && ((ax >> kRec2NearBit) & 1u)) {  // o = 256 P + lane offset >= base4 - piece0
+      const int64_t x = (int64_t)(c.base4 - piece0) - (int64_t)dma_off;
+      const int64_t pb = x <= 0 ? 0 : (x + 255) >> 8;
+      first = max(first, (int32_t)min(pb, (int64_t)0x40000000));
+    }
+    return first;
+  };
+  PairPlan p;
+  p.p0 = one(ax0, info0, p.db0);
+  p.p1 = one(ax1, info1, p.db1);
+  return p;
+}
+#endif
+
 // A pair round's per-lane state from its packet record and the round header (ns, B and
 // `fast` are wave-uniform, from the job build's per-round max / min step counts).
 __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t id,
@@ -1906,6 +1944,39 @@ __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint3
   rr.fast = fast;
   return rr;
 }
+
+#if ENET_CRC_REC2
+// pair_round_from_record from a round-relative record (no valid bit: an empty position, d = ns).
+__device__ __forceinline__ RaggedRound pair_round_from_record2(uint64_t ax, uint32_t info, bool rv,
+                                                               const LaneConsts& c, int32_t ns, int32_t B, bool fast,
+                                                               bool near_round) {
+  const uint64_t piece0 = ax & kRecAddrMask;
+  const uint32_t hi = (uint32_t)(ax >> 32);
+  const bool valid = rv && ((hi >> (kRec2ValidBit - 32)) & 1u);
+  const int32_t d = valid ? (int32_t)(info & kRecStepsMask) : ns;
+  const uint32_t pad = (info >> kRecPadShift) << 2;
+  RaggedRound rr;
+  rr.ns = ns;
+  rr.cb = piece0 + (uint64_t)(int64_t)(112 - 16 * (int32_t)c.k);  // = a1 - 16 (k + 1) - 128 (ns - 1)
+  rr.top_slot = d;
+  const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
+  const bool inside = d < ns && rel > -16;
+  bool fb = false;
+  if (near_round) {  // wave-uniform: only rounds holding a packet near the caller's base
+    if (((hi >> (kRec2NearBit - 32)) & 1u) && valid && inside && rel < 0) {
+      const uint64_t top = piece0 + (uint64_t)kBytesPerStep * (uint64_t)d + pad;
+      fb = top - c.base4 < (uint64_t)(-rel);
+    }
+  }
+  const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
+  rr.meta = head | ((hi >> 16) & kRec2MetaBits) | (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) |
+            (inside && !fb ? kMetaDirect : 0u);
+  rr.id = hi >> (kRec2LidShift - 32);
+  rr.top_uniform = B;
+  rr.fast = fast;
+  return rr;
+}
+#endif
 
 // Per-lane constants of the pair ring.
 struct PairRing {
@@ -2481,6 +2552,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                         (!partial || two_pairs);
       lds_st32(hdr + 16u * lane + 12u, (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u));
     }
+#if ENET_CRC_REC2
+    static_assert(ENET_CRC_HDR_PACKED, "the record rewrite reads the packed slot count");
+    // Round-relative records: lane l rewrites sorted positions 4 l .. 4 l + 3 (round l / 2)
+    // once the headers above are written (this wave's LDS operations are processed in order).
+    if (lane < 2u * RJ) {
+      const uint32_t rr = lane >> 1, e = 4u * (lane & 1u);
+      const uint32_t ra = st + rr * kJobRoundBytes + 8u * e, ri = st + rr * kJobRoundBytes + 64u + 4u * e;
+      const u32x4 a01 = lds_ld128(ra), a23 = lds_ld128(ra + 16u), iv = lds_ld128(ri);
+      const uint32_t ns = lds_ld32(hdr + 16u * rr + 12u) & kRecStepsMask;
+      const uint64_t a[4] = {a01.x | (uint64_t)a01.y << 32, a01.z | (uint64_t)a01.w << 32,
+                             a23.x | (uint64_t)a23.y << 32, a23.z | (uint64_t)a23.w << 32};
+      const uint32_t inf[4] = {iv.x, iv.y, iv.z, iv.w};
+      uint64_t a2[4];
+      uint32_t i2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool valid = (a[i] >> kRecValidBit) & 1u;
+        const uint32_t nsteps = inf[i] & kRecStepsMask;
+        const uint64_t piece0 = ((a[i] & kRecAddrMask) - (uint64_t)kBytesPerStep * ns) & kRecAddrMask;
+        const uint64_t flags = (1ull << kRec2ValidBit) | (((a[i] >> kRecNearBit) & 1ull) << kRec2NearBit) |
+                               (((a[i] >> kRecVShift) & 3ull) << (48 + kMetaVShift)) |
+                               ((nsteps == 0 ? 1ull : 0ull) << (48 + 5)) |
+                               (((a[i] >> kRecZShift) & 3ull) << (48 + kMetaNTailShift)) |
+                               (((a[i] >> kJobLidShift) & 255ull) << kRec2LidShift);
+        a2[i] = valid ? piece0 | flags : 0ull;
+        i2[i] = valid ? (ns - nsteps) | (inf[i] & ~kRecStepsMask) : ns;
+      }
+      asm volatile("ds_write_b128 %0, %1\n\tds_write_b128 %0, %2 offset:16\n\tds_write_b128 %3, %4\n\t"
+                   "s_waitcnt lgkmcnt(0)"
+                   :
+                   : "v"(ra), "v"(u32x4{(uint32_t)a2[0], (uint32_t)(a2[0] >> 32), (uint32_t)a2[1], (uint32_t)(a2[1] >> 32)}),
+                     "v"(u32x4{(uint32_t)a2[2], (uint32_t)(a2[2] >> 32), (uint32_t)a2[3], (uint32_t)(a2[3] >> 32)}),
+                     "v"(ri), "v"(u32x4{i2[0], i2[1], i2[2], i2[3]})
+                   : "memory");
+    }
+#endif
 #endif
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
   };
@@ -2646,7 +2753,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                       (!partial || ns == kPairMinSlots);
 #endif
     const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
-#if ENET_CRC_NEAR_SPLIT
+#if ENET_CRC_REC2
+    RaggedRound rr;
+    if (near_round) {
+      rr = pair_round_from_record2(ax, info, rv, c, ns, B, fast, true);
+      rr.plan = pair_plan2(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, true, c);
+    } else {
+      rr = pair_round_from_record2(ax, info, rv, c, ns, B, fast, false);
+      rr.plan = pair_plan2(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, false, c);
+    }
+#elif ENET_CRC_NEAR_SPLIT
     // Rounds holding a packet near the caller's base (the batch's first few) take their own copy
     // of the decode: the others carry no near-base code at all (one scalar branch).
     RaggedRound rr;
