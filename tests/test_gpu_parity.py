@@ -359,6 +359,33 @@ def test_ragged_mixed_class_rounds(dev, mix):
     assert np.array_equal(got, want), int(np.count_nonzero(got != want))
 
 
+# seeds chosen so that every draw kind (0-5) runs with and without overlapping packets
+@pytest.mark.parametrize("seed", [102, 136, 103, 172, 130, 129, 105, 107, 114, 115, 100, 101])
+def test_ragged_random_sweep(dev, seed):
+    """The randomized ragged sweep (scripts/fuzz_ragged.py: 120 batches / 18.0 M datagrams
+    bit-exact in round 5) as a regression guard: twelve seeded batches, each drawing a count,
+    a length distribution (uniform ranges, MTU fragments with short tails, tiny, bimodal,
+    128-B step edges, a long tail to 8 KiB; 2 % zero-length), gaps, overlapping re-reads and
+    a base offset 0-15, checked in full against the oracle."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "fuzz_ragged", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                                    "fuzz_ragged.py"))
+    fz = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fz)
+    rng = np.random.default_rng(seed)
+    kind, base, starts, lengths = fz.draw(rng)
+    if lengths.size > 120_000:  # keep the suite fast: the draw's own distribution, fewer packets
+        starts, lengths = starts[:120_000], lengths[:120_000]
+    total = int((starts + lengths.astype(np.uint64)).max()) + base + 8
+    data = rng.integers(0, 256, size=total, dtype=np.uint8)
+    got = ragged_on_device(data[base:], starts, lengths, dev)
+    want = _oracle.crc32_ragged(data[base:], starts, lengths, threads=8)
+    assert np.array_equal(got, want), (kind, base, int(np.count_nonzero(got != want)))
+
+
 # --- round-record scratch cached per stream (launch_ragged) ----------------------------------
 
 def test_ragged_scratch_per_stream(dev):
