@@ -14,6 +14,7 @@
 //   16x128x2 d1  two 8x128 instructions per slot, one slot in flight
 //   8x128 regs   the 8-lane shape loaded into a register ring (3 or 6 deep; nt: non-temporal)
 //   8x256x2 d2/3 8 packets x 256 B per 2-KiB slot as two 4 x 256-B instructions (the round-5 plan)
+//   4x256x1 d4, 8x256x2 d1, 4x512x2 d2, 2x512x1 d4: the same bytes in flight with other packet counts
 // Workgroups of 1024 threads, one per CU (the LDS is padded to the kernels' 150 KiB), a
 // persistent grid over static rounds.  Alternating blocks of 20 launches per shape after a
 // warm-up; prints us per launch and GB/s.  Addresses stay inside the buffer: the packets
@@ -205,6 +206,9 @@ int main(int argc, char** argv) {
       {"8x256x2 d2", 8, launch_shape<8, 256, 2, 2>},   {"8x256x2 d3", 8, launch_shape<8, 256, 2, 3>},
       {"8x128 regs d3", 8, launch_regs<8, 128, 3, false>}, {"8x128 regs d6", 8, launch_regs<8, 128, 6, false>},
       {"8x128 regsnt d6", 8, launch_regs<8, 128, 6, true>},
+      // round-5 additions: in-flight bytes vs packets per wave
+      {"4x256x1 d4", 4, launch_shape<4, 256, 1, 4>},   {"8x256x2 d1", 8, launch_shape<8, 256, 2, 1>},
+      {"4x512x2 d2", 4, launch_shape<4, 512, 2, 2>},   {"2x512x1 d4", 2, launch_shape<2, 512, 1, 4>},
   };
   const int ns = sizeof(shapes) / sizeof(shapes[0]);
   hipDeviceProp_t prop;
