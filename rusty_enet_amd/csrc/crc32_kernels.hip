@@ -1801,6 +1801,9 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
 // flight.  The DMA lane decides per 16-B chunk whether it is real (at or after its packet's
 // top word, not below the caller's buffer) or the zero chunk.
 // ---------------------------------------------------------------------------------
+#ifndef ENET_CRC_STAGGER
+#define ENET_CRC_STAGGER 0  // staggered pair refills (measurement switch; see pair_step)
+#endif
 constexpr int kPairRing = 2;                                    // pair slots per wave
 // Lane k == 0 clears the z bytes past its packet's end in the last word (z in meta).
 __device__ __forceinline__ uint32_t last_word_mask(uint32_t meta, uint32_t k) {
@@ -2008,6 +2011,23 @@ struct PairRing {
     __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 0);
 #endif
   }
+#if ENET_CRC_STAGGER
+  // One of the two DMAs of pair P (I = 0: packets 0-3, I = 1: packets 4-7).
+  template <int I>
+  __device__ __forceinline__ void issue_one(const PairPlan& pl, int32_t P, uint32_t slot, bool checked,
+                                            const LaneConsts& c) {
+    const uint64_t o = 256u * (uint64_t)P;
+    uint64_t src = (I == 0 ? pl.db0 : pl.db1) + o;
+    if (checked) src = P >= (I == 0 ? pl.p0 : pl.p1) ? src : c.dummy;
+    LdsChar* const dst = (LdsChar*)slot0 + slot * kPairStride + 1024u * I;
+#ifdef ENET_CRC_ABL_NODMA
+    if (src == 0) __builtin_trap();
+    (void)dst;
+#else
+    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)dst, 16, 0, 0);
+#endif
+  }
+#endif
   __device__ __forceinline__ uint32_t addr_a(uint32_t slot) const { return ring0 + slot * kPairStride + rd_a; }
   __device__ __forceinline__ uint32_t addr_b(uint32_t slot) const { return ring0 + slot * kPairStride + (rd_a ^ 128u); }
 };
@@ -2030,6 +2050,63 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
 #else
   constexpr int kWait = 2;
 #endif
+#if ENET_CRC_STAGGER
+  // Staggered refills: the two DMAs of pair P + 2 go out one compute slot apart (the first
+  // after half 0 of pair P, the second after half 1), so a wave has 1-3 DMAs in flight instead
+  // of 2-4 and issues them one at a time.  Consuming half 1 of pair P reads pair P + 1's first
+  // half: in flight then are P + 1's two DMAs and P + 2's first, so vmcnt(1).  Half 0 reads
+  // its own pair's second half, landed before half 0 began (vmcnt(2) never waits).
+  constexpr int kWaitH1 = kWait == 2 ? 1 : kWait;
+  if (half0) {
+#ifdef ENET_CRC_ABL_NOLOOKUP
+    if constexpr (kLook) {
+      h0 ^= w0;
+      h1 ^= w1;
+      h2 ^= w2;
+      h3 ^= w3;
+    }
+    R.nextv = read_landed_slot<kWait>(next_addr);
+#else
+    if constexpr (kLook) {
+      horner_step_and_read<kWait>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
+    } else {
+      R.nextv = read_landed_slot<kWait>(next_addr);
+    }
+#endif
+  } else {
+#ifdef ENET_CRC_ABL_NOLOOKUP
+    if constexpr (kLook) {
+      h0 ^= w0;
+      h1 ^= w1;
+      h2 ^= w2;
+      h3 ^= w3;
+    }
+    R.nextv = read_landed_slot<kWaitH1>(next_addr);
+#else
+    if constexpr (kLook) {
+      horner_step_and_read<kWaitH1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
+    } else {
+      R.nextv = read_landed_slot<kWaitH1>(next_addr);
+    }
+#endif
+  }
+  {
+    const int32_t f = s / 2 + kPairRing, np = ns / 2;  // the pair that refills pair slot R.q
+    if (half0) {
+      if (f < np)
+        R.issue_one<0>(cur, f, R.q, cur_checked, c);
+      else
+        R.issue_one<0>(nxt, f - np, R.q, true, c);
+    } else {
+      if (f < np)
+        R.issue_one<1>(cur, f, R.q, cur_checked, c);
+      else
+        R.issue_one<1>(nxt, f - np, R.q, true, c);
+      R.q ^= 1u;
+    }
+  }
+}
+#else
 #ifdef ENET_CRC_ABL_NOLOOKUP  // ablation: the slot's data XORed into the streams, no table lookups
   if constexpr (kLook) {
     h0 ^= w0;
@@ -2055,6 +2132,7 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
     R.q ^= 1u;
   }
 }
+#endif
 
 // A fast round (tops of every packet in compute slots T .. T + 1, or T .. 3 when NS = 4; no
 // fallback): unrolled; the pairs it issues for itself (P >= 2) need no check.

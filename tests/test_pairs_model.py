@@ -228,3 +228,65 @@ def test_pair_ring_sequence():
                         issue(r + 1, f - ns // 2, q)
                 else:
                     q ^= 1
+
+
+def test_pair_ring_sequence_staggered():
+    """The staggered refill (ENET_CRC_STAGGER, pair_step): the two DMAs of a refill pair go out
+    one compute slot apart (instruction 0 after half 0, instruction 1 after half 1, both into the
+    pair slot just emptied).  Checked per DMA instruction across a wave's rounds, with the
+    descriptor DMAs of a job build (3 per build) issued at random round starts: each compute
+    read finds both DMAs of its pair landed after its wait (vmcnt(2) at half 0, vmcnt(1) at
+    half 1; DMAs complete in issue order), no pair slot half is refilled before its last read,
+    and at every round end the same DMAs are in flight as with whole-pair refills (the next
+    round's pair 1), which the job build's own waits count on."""
+    rng = np.random.default_rng(11)
+    for _ in range(300):
+        rounds = [2 * int(x) for x in rng.integers(2, 8, size=int(rng.integers(1, 12)))] + [4]
+        dmas = []          # issue order: ("ring", round, pair, instr) or ("job",)
+        slot_of = {}       # (round, pair) -> pair slot
+        reads_left = {}    # (round, pair) -> reads of that pair still to come (2 halves)
+
+        def issue(r, P, i, q):
+            if i == 0:
+                assert all(v == 0 for k, v in reads_left.items() if slot_of.get(k) == q), ("refilled early", r, P)
+                slot_of[(r, P)] = q
+                reads_left[(r, P)] = 2
+            else:
+                assert slot_of[(r, P)] == q
+            dmas.append(("ring", r, P, i))
+
+        def wait(n):  # vmcnt(n): everything but the last n issued has landed
+            return set(dmas[:-n] if n else dmas)
+
+        def need(r, P, landed):
+            assert ("ring", r, P, 0) in landed and ("ring", r, P, 1) in landed, ("not landed", r, P)
+
+        for i in range(2):
+            issue(0, 0, i, 0)
+        for i in range(2):
+            issue(0, 1, i, 1)
+        need(0, 0, wait(2))
+        reads_left[(0, 0)] -= 1
+        q = 0
+        for r in range(len(rounds) - 1):
+            ns = rounds[r]
+            if rng.random() < 0.3:  # a job build's descriptor DMAs at the round's start
+                dmas.extend([("job",)] * 3)
+            if r > 0:  # round end invariant: the next round's pair 1 is what is in flight
+                ring_tail = [d for d in dmas if d[0] == "ring"][-2:]
+                assert ring_tail == [("ring", r, 1, 0), ("ring", r, 1, 1)], ring_tail
+            for s in range(ns):
+                P, half = s >> 1, s & 1
+                f = P + 2
+                tgt = (r, f) if f < ns // 2 else (r + 1, f - ns // 2)
+                if half == 0:
+                    need(r, P, wait(2))           # reading half 1 of pair P
+                    reads_left[(r, P)] -= 1
+                    issue(tgt[0], tgt[1], 0, q)
+                else:
+                    nxt = (r + 1, 0) if s == ns - 1 else (r, P + 1)
+                    assert slot_of[nxt] == q ^ 1
+                    need(nxt[0], nxt[1], wait(1))  # reading half 0 of the next pair
+                    reads_left[nxt] -= 1
+                    issue(tgt[0], tgt[1], 1, q)
+                    q ^= 1
