@@ -712,8 +712,10 @@ constexpr int kRecPadShift = 26;
 // A position past the job: ax = 0, info = ns.  Readers take d = ns (never real) whenever the
 // valid bit is clear -- also for the all-zero record of a round that is not live.  (Device and
 // host virtual addresses here are far above 128 ns <= 8 GiB, so piece0 never wraps.)
+#if ENET_CRC_REC2
 constexpr int kRec2ValidBit = 48, kRec2NearBit = 49, kRec2LidShift = 56;
 constexpr uint32_t kRec2MetaBits = 0xF8u;  // (ax >> 48) & this = v | empty | z in meta layout
+#endif
 
 struct RaggedRecord {
   uint64_t ax;
