@@ -378,10 +378,6 @@ __device__ __forceinline__ uint32_t combine_tree(const uint32_t* lds, uint32_t h
   return y;
 }
 
-#ifndef ENET_CRC_TREE_ASM  // jobs kernel: the tree levels as one asm statement (0: combine_tree, A/B builds)
-#define ENET_CRC_TREE_ASM 1
-#endif
-#if ENET_CRC_TREE_ASM
 // combine_tree's three tree levels for a kernel whose tables start at LDS address 0 (the
 // unreplicated tree sets at kTreeDword, byte 0x10000).  Each lookup address is ONE
 // v_lshlrev_b32_sdwa: byte j of y, times 4, written into the low half of `a`, whose high half
@@ -426,7 +422,6 @@ __device__ __forceinline__ uint32_t tree_levels_asm(uint32_t y, uint32_t& a) {
   return y;
 }
 #undef ENET_TREE_LEVEL
-#endif
 
 // combine_tree for the register-ring kernel's layout (kRegsLdsDwords): the first two tree
 // levels through the replicated tree block (conflict-free), the third unreplicated.
@@ -704,19 +699,6 @@ constexpr uint64_t kRecAddrMask = (1ull << 48) - 1;
 constexpr int kRecVShift = 48, kRecZShift = 50, kRecNearBit = 52, kRecValidBit = 53;
 constexpr uint32_t kRecStepsMask = (1u << 26) - 1;
 constexpr int kRecPadShift = 26;
-// Round-relative records (ENET_CRC_REC2: the job build's last pass, once the round's slot
-// count ns is known):
-//   ax   (u64): piece0 = a1 - 128 ns (48 bits) | valid << 48 | near << 49 | v << 51 |
-//               empty << 53 | z << 54 | local id << 56   (v, empty, z at their meta positions + 48)
-//   info (u32): d = ns - nsteps (the packet's top slot) | (pad / 4) << 26
-// A position past the job: ax = 0, info = ns.  Readers take d = ns (never real) whenever the
-// valid bit is clear -- also for the all-zero record of a round that is not live.  (Device and
-// host virtual addresses here are far above 128 ns <= 8 GiB, so piece0 never wraps.)
-#if ENET_CRC_REC2
-constexpr int kRec2ValidBit = 48, kRec2NearBit = 49, kRec2LidShift = 56;
-constexpr uint32_t kRec2MetaBits = 0xF8u;  // (ax >> 48) & this = v | empty | z in meta layout
-#endif
-
 struct RaggedRecord {
   uint64_t ax;
   uint32_t info;
@@ -792,29 +774,6 @@ typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
 #ifndef ENET_CRC_RAGGED_PAIRS  // ragged jobs kernel: 256-B pair loads; 0: the round-4 loads (A/B builds)
 #define ENET_CRC_RAGGED_PAIRS 1
-#endif
-#ifndef ENET_CRC_DIET  // jobs kernel: fewer instructions per round (top-chunk masks from an LDS table, the
-                       // checksum store and the last-word mask without lane compares); A/B builds
-#define ENET_CRC_DIET 1
-#endif
-#ifndef ENET_CRC_HDR_PACKED  // jobs kernel: the job build packs each round's slot count, first top and
-                             // fast flag into its header (A/B builds)
-#define ENET_CRC_HDR_PACKED 1
-#endif
-#ifndef ENET_CRC_NEAR_SPLIT  // jobs kernel: near-base rounds decoded by their own copy (A/B builds)
-#define ENET_CRC_NEAR_SPLIT 1
-#endif
-#ifndef ENET_CRC_LANE0_ATOMICS  // jobs kernel: wave-level LDS counter updates without an EXEC change (A/B)
-#define ENET_CRC_LANE0_ATOMICS 0
-#endif
-#ifndef ENET_CRC_REC2  // jobs kernel: the job build rewrites each record relative to its round (A/B)
-#define ENET_CRC_REC2 0
-#endif
-#ifndef ENET_CRC_MERGED_FLAGS  // jobs kernel: ready / freed flags read with the round's records (A/B)
-#define ENET_CRC_MERGED_FLAGS 0
-#endif
-#ifndef ENET_CRC_CLAIM_BATCH  // ragged jobs kernel: rounds claimed per LDS atomic (A/B builds: 2, 4)
-#define ENET_CRC_CLAIM_BATCH 1
 #endif
 #ifndef ENET_CRC_RAGGED_RING
 #define ENET_CRC_RAGGED_RING 3  // A/B variants may build 4 (with ENET_CRC_JOB_SLOTS=4 for the LDS)
@@ -1803,23 +1762,15 @@ __device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, con
 // flight.  The DMA lane decides per 16-B chunk whether it is real (at or after its packet's
 // top word, not below the caller's buffer) or the zero chunk.
 // ---------------------------------------------------------------------------------
-#ifndef ENET_CRC_STAGGER
-#define ENET_CRC_STAGGER 0  // staggered pair refills (measurement switch; see pair_step)
-#endif
 constexpr int kPairRing = 2;                                    // pair slots per wave
 // Lane k == 0 clears the z bytes past its packet's end in the last word (z in meta).
 __device__ __forceinline__ uint32_t last_word_mask(uint32_t meta, uint32_t k) {
-#if ENET_CRC_DIET
   // No lane compare (hipcc hoists k == 0 into a lane mask, then spills it to a VGPR lane):
   // kz = 0x18 on lane k == 0, else 0, by an arithmetic shift; the shift is 8 z there, else 0.
   const uint32_t kz = 0x18u & (uint32_t)((int32_t)(k - 1u) >> 31);
   return 0xFFFFFFFFu >> ((meta >> (kMetaNTailShift - 3)) & kz);
-#else
-  return k == 0 ? 0xFFFFFFFFu >> (8u * ((meta >> kMetaNTailShift) & 3u)) : 0xFFFFFFFFu;
-#endif
 }
 
-#if ENET_CRC_DIET
 // Top-chunk masks from a 32-entry LDS table indexed by meta's head and v fields (5 bits):
 // entry e = {m0..m3}, {x0..x3} with w_i <- (w_i & m_i) ^ x_i (mask_top's words, the initial
 // register injected into the top word).  One asm statement: hipcc would put a plain LDS read
@@ -1861,7 +1812,6 @@ __device__ __forceinline__ void mask_top_lds(uint32_t meta, uint32_t table, uint
   w2 = __builtin_amdgcn_bitop3_b32(w2, m.z, x.z, 0x6A);
   w3 = __builtin_amdgcn_bitop3_b32(w3, m.w, x.w, 0x6A);
 }
-#endif
 constexpr uint32_t kPairBytes = 2048;                           // one pair slot of one wave
 constexpr uint32_t kPairStride = kWavesPerBlock * kPairBytes;   // bytes between ring positions
 constexpr int kPairMinSlots = 2 * kPairRing;                    // a round's first 2 pairs come from the round before
@@ -1893,30 +1843,6 @@ __device__ __forceinline__ PairPlan pair_plan(uint64_t ax0, uint32_t info0, uint
   return p;
 }
 
-#if ENET_CRC_REC2
-// pair_plan from round-relative records: piece0 and d come stored.  A record without the valid
-// bit (a position past the job, or the zeros of a round that is not live) is never real.
-__device__ __forceinline__ PairPlan pair_plan2(uint64_t ax0, uint32_t info0, uint64_t ax1, uint32_t info1, int32_t ns,
-                                               uint32_t dma_off, bool near_round, const LaneConsts& c) {
-  auto one = [&](uint64_t ax, uint32_t info, uint64_t& db) -> int32_t {
-    const uint64_t piece0 = ax & kRecAddrMask;
-    db = piece0 + dma_off;
-    const bool valid = (ax >> kRec2ValidBit) & 1u;
-    const uint32_t d = valid ? info & kRecStepsMask : (uint32_t)ns, pad = (info >> kRecPadShift) << 2;
-    int32_t first = (int32_t)((d >> 1) + ((128u * (d & 1u) + pad + 240u - dma_off) >> 8));
-    if (near_round && ((ax >> kRec2NearBit) & 1u)) {  // o = 256 P + lane offset >= base4 - piece0
-      const int64_t x = (int64_t)(c.base4 - piece0) - (int64_t)dma_off;
-      const int64_t pb = x <= 0 ? 0 : (x + 255) >> 8;
-      first = max(first, (int32_t)min(pb, (int64_t)0x40000000));
-    }
-    return first;
-  };
-  PairPlan p;
-  p.p0 = one(ax0, info0, p.db0);
-  p.p1 = one(ax1, info1, p.db1);
-  return p;
-}
-#endif
 
 // A pair round's per-lane state from its packet record and the round header (ns, B and
 // `fast` are wave-uniform, from the job build's per-round max / min step counts).
@@ -1950,44 +1876,10 @@ __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint3
   return rr;
 }
 
-#if ENET_CRC_REC2
-// pair_round_from_record from a round-relative record (no valid bit: an empty position, d = ns).
-__device__ __forceinline__ RaggedRound pair_round_from_record2(uint64_t ax, uint32_t info, bool rv,
-                                                               const LaneConsts& c, int32_t ns, int32_t B, bool fast,
-                                                               bool near_round) {
-  const uint64_t piece0 = ax & kRecAddrMask;
-  const uint32_t hi = (uint32_t)(ax >> 32);
-  const bool valid = rv && ((hi >> (kRec2ValidBit - 32)) & 1u);
-  const int32_t d = valid ? (int32_t)(info & kRecStepsMask) : ns;
-  const uint32_t pad = (info >> kRecPadShift) << 2;
-  RaggedRound rr;
-  rr.ns = ns;
-  rr.cb = piece0 + (uint64_t)(int64_t)(112 - 16 * (int32_t)c.k);  // = a1 - 16 (k + 1) - 128 (ns - 1)
-  rr.top_slot = d;
-  const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
-  const bool inside = d < ns && rel > -16;
-  bool fb = false;
-  if (near_round) {  // wave-uniform: only rounds holding a packet near the caller's base
-    if (((hi >> (kRec2NearBit - 32)) & 1u) && valid && inside && rel < 0) {
-      const uint64_t top = piece0 + (uint64_t)kBytesPerStep * (uint64_t)d + pad;
-      fb = top - c.base4 < (uint64_t)(-rel);
-    }
-  }
-  const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
-  rr.meta = head | ((hi >> 16) & kRec2MetaBits) | (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) |
-            (inside && !fb ? kMetaDirect : 0u);
-  rr.id = hi >> (kRec2LidShift - 32);
-  rr.top_uniform = B;
-  rr.fast = fast;
-  return rr;
-}
-#endif
 
 // Per-lane constants of the pair ring.
 struct PairRing {
-#if ENET_CRC_DIET
   uint32_t topmask;  // LDS address of the top-chunk mask table (mask_top_lds)
-#endif
   LdsVoid* slot0;    // this wave's pair slot 0
   uint32_t ring0;    // its LDS byte address
   uint32_t rd_a;     // this lane's read offset, half 0 (compute slot 2P)
@@ -2013,23 +1905,6 @@ struct PairRing {
     __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 0);
 #endif
   }
-#if ENET_CRC_STAGGER
-  // One of the two DMAs of pair P (I = 0: packets 0-3, I = 1: packets 4-7).
-  template <int I>
-  __device__ __forceinline__ void issue_one(const PairPlan& pl, int32_t P, uint32_t slot, bool checked,
-                                            const LaneConsts& c) {
-    const uint64_t o = 256u * (uint64_t)P;
-    uint64_t src = (I == 0 ? pl.db0 : pl.db1) + o;
-    if (checked) src = P >= (I == 0 ? pl.p0 : pl.p1) ? src : c.dummy;
-    LdsChar* const dst = (LdsChar*)slot0 + slot * kPairStride + 1024u * I;
-#ifdef ENET_CRC_ABL_NODMA
-    if (src == 0) __builtin_trap();
-    (void)dst;
-#else
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)dst, 16, 0, 0);
-#endif
-  }
-#endif
   __device__ __forceinline__ uint32_t addr_a(uint32_t slot) const { return ring0 + slot * kPairStride + rd_a; }
   __device__ __forceinline__ uint32_t addr_b(uint32_t slot) const { return ring0 + slot * kPairStride + (rd_a ^ 128u); }
 };
@@ -2052,63 +1927,6 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
 #else
   constexpr int kWait = 2;
 #endif
-#if ENET_CRC_STAGGER
-  // Staggered refills: the two DMAs of pair P + 2 go out one compute slot apart (the first
-  // after half 0 of pair P, the second after half 1), so a wave has 1-3 DMAs in flight instead
-  // of 2-4 and issues them one at a time.  Consuming half 1 of pair P reads pair P + 1's first
-  // half: in flight then are P + 1's two DMAs and P + 2's first, so vmcnt(1).  Half 0 reads
-  // its own pair's second half, landed before half 0 began (vmcnt(2) never waits).
-  constexpr int kWaitH1 = kWait == 2 ? 1 : kWait;
-  if (half0) {
-#ifdef ENET_CRC_ABL_NOLOOKUP
-    if constexpr (kLook) {
-      h0 ^= w0;
-      h1 ^= w1;
-      h2 ^= w2;
-      h3 ^= w3;
-    }
-    R.nextv = read_landed_slot<kWait>(next_addr);
-#else
-    if constexpr (kLook) {
-      horner_step_and_read<kWait>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
-    } else {
-      R.nextv = read_landed_slot<kWait>(next_addr);
-    }
-#endif
-  } else {
-#ifdef ENET_CRC_ABL_NOLOOKUP
-    if constexpr (kLook) {
-      h0 ^= w0;
-      h1 ^= w1;
-      h2 ^= w2;
-      h3 ^= w3;
-    }
-    R.nextv = read_landed_slot<kWaitH1>(next_addr);
-#else
-    if constexpr (kLook) {
-      horner_step_and_read<kWaitH1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
-    } else {
-      R.nextv = read_landed_slot<kWaitH1>(next_addr);
-    }
-#endif
-  }
-  {
-    const int32_t f = s / 2 + kPairRing, np = ns / 2;  // the pair that refills pair slot R.q
-    if (half0) {
-      if (f < np)
-        R.issue_one<0>(cur, f, R.q, cur_checked, c);
-      else
-        R.issue_one<0>(nxt, f - np, R.q, true, c);
-    } else {
-      if (f < np)
-        R.issue_one<1>(cur, f, R.q, cur_checked, c);
-      else
-        R.issue_one<1>(nxt, f - np, R.q, true, c);
-      R.q ^= 1u;
-    }
-  }
-}
-#else
 #ifdef ENET_CRC_ABL_NOLOOKUP  // ablation: the slot's data XORed into the streams, no table lookups
   if constexpr (kLook) {
     h0 ^= w0;
@@ -2134,7 +1952,6 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
     R.q ^= 1u;
   }
 }
-#endif
 
 // A fast round (tops of every packet in compute slots T .. T + 1, or T .. 3 when NS = 4; no
 // fallback): unrolled; the pairs it issues for itself (P >= 2) need no check.
@@ -2158,11 +1975,7 @@ __device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const Pa
     if (s <= kMaskEnd) {
       const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
       if (__builtin_amdgcn_ballot_w64(mine)) {
-#if ENET_CRC_DIET
         if (mine) mask_top_lds(cur.meta, R.topmask, w0, w1, w2, w3);
-#else
-        if (mine) mask_top(cur.meta, w0, w1, w2, w3);
-#endif
       }
     }
     if (s == T) {
@@ -2221,11 +2034,7 @@ __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const
     }
     if (s == cur.ns - 1) w3 &= last_word_mask(cur.meta, c.k);
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
-#if ENET_CRC_DIET
       if (top && (cur.meta & kMetaHeadMask)) mask_top_lds(cur.meta, R.topmask, w0, w1, w2, w3);
-#else
-      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
-#endif
     }
     h0 = horner_main(lds, h0, w0, c.lk);
     h1 = horner_main(lds, h1, w1, c.lk);
@@ -2303,10 +2112,8 @@ struct RaggedJobsLds {
   uint32_t freed[kJobSlots];     // k + 1 once the k-th job's checksums are in HBM
   uint32_t next_dispatch;
   uint32_t failed;               // != 0 once a wave gave up a wait: later waits fail at once, nothing more is flushed
-#if ENET_CRC_DIET
   TopMaskEntry topmask[32];      // mask_top_lds
   uint32_t res_dummy[64];        // publish(): where the lanes that hold no checksum store theirs
-#endif
 };
 static_assert(sizeof(RaggedJobsLds) <= 160 * 1024, "LDS");
 
@@ -2356,23 +2163,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(
 __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
-#if ENET_CRC_LANE0_ATOMICS
-// A counter update of the wave (lane 0's), issued by every lane: lane 0 adds v to the counter,
-// the others add 0 to their own word of a dummy row (64 distinct words: no conflicts, no
-// serialisation), so no lane compare and no EXEC change is needed.  l0 = all ones on lane 0
-// (a per-lane constant), drow = the lane's word of the dummy row.
-__device__ __forceinline__ uint32_t lds_add_rtn_l0(uint32_t a, uint32_t v, uint32_t l0, uint32_t drow) {
-  uint32_t old;
-  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
-               : "=v"(old)
-               : "v"((l0 & a) | (~l0 & drow)), "v"(l0 & v)
-               : "memory");
-  return __builtin_amdgcn_readfirstlane(old);
-}
-__device__ __forceinline__ void lds_add_nowait_l0(uint32_t a, uint32_t v, uint32_t l0, uint32_t drow) {
-  asm volatile("ds_add_u32 %0, %1" : : "v"((l0 & a) | (~l0 & drow)), "v"(l0 & v) : "memory");
-}
-#endif
 #if ENET_CRC_RAGGED_PAIRS
 __device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
@@ -2457,20 +2247,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     S.next_dispatch = kWavesPerBlock * kLook;
     S.failed = 0;
   }
-#if ENET_CRC_DIET
   fill_top_masks(S.topmask);
-#endif
   fill_lds(lds);
   __syncthreads();
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
-#if ENET_CRC_LANE0_ATOMICS
-  static_assert(ENET_CRC_DIET, "the dummy row is res_dummy");
-  const uint32_t l0 = (uint32_t)((int32_t)(lane - 1u) >> 31);  // all ones on lane 0
-  const uint32_t drow = lds_addr(&S.res_dummy[0]) + 4u * lane;
-#endif
 
   auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
   const uint32_t JP = b.job_packets;
@@ -2492,7 +2275,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint64_t J = job_of(k);
     return J < b.njobs && (uint64_t)(d - k * RJ) * kPacketsPerWave < job_count(J);
   };
-#if ENET_CRC_DIET
   // This workgroup's jobs k = 0 .. wg_jobs - 1 (job J = blockIdx.x + k grid); only its last can
   // hold fewer than JP packets.  Per round then: live = d < wg_rounds, and the job's packet and
   // round counts by one scalar compare (no 64-bit job arithmetic per round).
@@ -2500,7 +2282,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   const uint32_t last_n = job_count(job_of(wg_jobs - 1u));
   const uint32_t last_rounds = (last_n + kPacketsPerWave - 1) / kPacketsPerWave;
   const uint32_t wg_rounds = (wg_jobs - 1u) * RJ + last_rounds;
-#endif
 
   // Phase A: the descriptors of job J into the slot's record area (u64 offsets at +0,
   // u32 lengths at +2048): three 16-B DMAs per lane (kJobPackets descriptors from the
@@ -2617,7 +2398,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       }
 #endif
     }
-#if ENET_CRC_RAGGED_PAIRS && ENET_CRC_HDR_PACKED
+#if ENET_CRC_RAGGED_PAIRS
     // Per round, make_round's rule evaluated once here: hdr.w = ns | B << 26 | fast << 31 (the
     // header's max / min / near are complete: this wave's LDS atomics above are processed
     // before its read below).
@@ -2632,42 +2413,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                         (!partial || two_pairs);
       lds_st32(hdr + 16u * lane + 12u, (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u));
     }
-#if ENET_CRC_REC2
-    static_assert(ENET_CRC_HDR_PACKED, "the record rewrite reads the packed slot count");
-    // Round-relative records: lane l rewrites sorted positions 4 l .. 4 l + 3 (round l / 2)
-    // once the headers above are written (this wave's LDS operations are processed in order).
-    if (lane < 2u * RJ) {
-      const uint32_t rr = lane >> 1, e = 4u * (lane & 1u);
-      const uint32_t ra = st + rr * kJobRoundBytes + 8u * e, ri = st + rr * kJobRoundBytes + 64u + 4u * e;
-      const u32x4 a01 = lds_ld128(ra), a23 = lds_ld128(ra + 16u), iv = lds_ld128(ri);
-      const uint32_t ns = lds_ld32(hdr + 16u * rr + 12u) & kRecStepsMask;
-      const uint64_t a[4] = {a01.x | (uint64_t)a01.y << 32, a01.z | (uint64_t)a01.w << 32,
-                             a23.x | (uint64_t)a23.y << 32, a23.z | (uint64_t)a23.w << 32};
-      const uint32_t inf[4] = {iv.x, iv.y, iv.z, iv.w};
-      uint64_t a2[4];
-      uint32_t i2[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool valid = (a[i] >> kRecValidBit) & 1u;
-        const uint32_t nsteps = inf[i] & kRecStepsMask;
-        const uint64_t piece0 = ((a[i] & kRecAddrMask) - (uint64_t)kBytesPerStep * ns) & kRecAddrMask;
-        const uint64_t flags = (1ull << kRec2ValidBit) | (((a[i] >> kRecNearBit) & 1ull) << kRec2NearBit) |
-                               (((a[i] >> kRecVShift) & 3ull) << (48 + kMetaVShift)) |
-                               ((nsteps == 0 ? 1ull : 0ull) << (48 + 5)) |
-                               (((a[i] >> kRecZShift) & 3ull) << (48 + kMetaNTailShift)) |
-                               (((a[i] >> kJobLidShift) & 255ull) << kRec2LidShift);
-        a2[i] = valid ? piece0 | flags : 0ull;
-        i2[i] = valid ? (ns - nsteps) | (inf[i] & ~kRecStepsMask) : ns;
-      }
-      asm volatile("ds_write_b128 %0, %1\n\tds_write_b128 %0, %2 offset:16\n\tds_write_b128 %3, %4\n\t"
-                   "s_waitcnt lgkmcnt(0)"
-                   :
-                   : "v"(ra), "v"(u32x4{(uint32_t)a2[0], (uint32_t)(a2[0] >> 32), (uint32_t)a2[1], (uint32_t)(a2[1] >> 32)}),
-                     "v"(u32x4{(uint32_t)a2[2], (uint32_t)(a2[2] >> 32), (uint32_t)a2[3], (uint32_t)(a2[3] >> 32)}),
-                     "v"(ri), "v"(u32x4{i2[0], i2[1], i2[2], i2[3]})
-                   : "memory");
-    }
-#endif
 #endif
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
   };
@@ -2706,80 +2451,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     uint64_t ax = 0;
     uint32_t info = 0;
     const uint32_t k = div_rj(d), slot = k % kJobSlots;
-#if ENET_CRC_DIET
     const bool live = d < wg_rounds;  // round_valid(d)
     const uint32_t n = k + 1u == wg_jobs ? last_n : JP;
-#else
-    const uint64_t J = job_of(k);
-    const uint32_t n = J < b.njobs ? job_count(J) : 0u;
-    const bool live = (d - k * RJ) * kPacketsPerWave < n;  // round_valid(d)
-#endif
     bool rv = live;
-#if ENET_CRC_MERGED_FLAGS && ENET_CRC_RAGGED_PAIRS
-    u32x4 axd = {0, 0, 0, 0};  // the records of this lane's DMA packets lane / 16 and lane / 16 + 4
-    uint64_t infod = 0;
-    u32x4 hd = {0, 0, 0, 0};   // the round header: max steps, min steps, near flag
-    const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
-    const uint32_t gd = lane >> 4;
-    auto read_records = [&]() {
-      asm volatile(  // one round trip
-          "ds_read_b64 %0, %5\n\tds_read_b32 %1, %6\n\t"
-          "ds_read2_b64 %2, %7 offset1:4\n\tds_read2_b32 %3, %8 offset1:4\n\t"
-          "ds_read_b128 %4, %9\n\ts_waitcnt lgkmcnt(0)"
-          : "=&v"(ax), "=&v"(info), "=&v"(axd), "=&v"(infod), "=&v"(hd)
-          : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(r + 64u + 4u * gd),
-            "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
-          : "memory");
-    };
-    // The job's ready flag and its slot's freed flag ride in the records' round trip: LDS
-    // operations are processed in order, so records read after a ready flag that reads set are
-    // the built ones (the builder stores them before the flag).  Only a flag that is not set
-    // yet costs a wait and a second read.
-    if (rv) {
-      uint32_t rdy, frd;
-      asm volatile(
-          "ds_read_b32 %5, %10\n\tds_read_b32 %6, %11\n\t"
-          "ds_read_b64 %0, %7\n\tds_read_b32 %1, %8\n\t"
-          "ds_read2_b64 %2, %9 offset1:4\n\tds_read2_b32 %3, %12 offset1:4\n\t"
-          "ds_read_b128 %4, %13\n\ts_waitcnt lgkmcnt(0)"
-          : "=&v"(ax), "=&v"(info), "=&v"(axd), "=&v"(infod), "=&v"(hd), "=&v"(rdy), "=&v"(frd)
-          : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(lds_addr(&S.ready[slot])),
-            "v"(lds_addr(&S.freed[slot])), "v"(r + 64u + 4u * gd),
-            "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
-          : "memory");
-      if (k + 1u > seen_ready) {
-        if (__builtin_amdgcn_readfirstlane(rdy) == k + 1u) {
-          seen_ready = k + 1u;
-        } else {
-          rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a SPIN_ACC(spin_ready)), kFaultReady);
-          if (rv) {
-            seen_ready = k + 1u;
-            read_records();
-          }
-        }
-      }
-      // publish() of this job waits for the slot's previous job to be flushed: seen already?
-      if (k >= (uint32_t)kJobSlots && k + 1u - (uint32_t)kJobSlots > seen_freed &&
-          __builtin_amdgcn_readfirstlane(frd) == k + 1u - (uint32_t)kJobSlots)
-        seen_freed = k + 1u - (uint32_t)kJobSlots;
-    }
-#ifdef ENET_CRC_TEST_HOOKS
-    if (rv && blockIdx.x == 0 && k + 1u == b.fault_k && b.fault_kind == kFaultReady) rv = waited(kWaitGaveUp, kFaultReady);
-#endif
-    if (rv) {
-#if ENET_CRC_LANE0_ATOMICS
-      lds_add_nowait_l0(lds_addr(&S.consumed[slot]), 1u, l0, drow);
-#else
-      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
-#endif
-    } else {
-      ax = 0;
-      info = 0;
-      axd = u32x4{0, 0, 0, 0};
-      infod = 0;
-      hd = u32x4{0, 0, 0, 0};
-    }
-#else
     if (rv && k + 1u > seen_ready) {
       rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a SPIN_ACC(spin_ready)), kFaultReady);
       if (rv) seen_ready = k + 1u;
@@ -2802,47 +2476,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
           : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(r + 64u + 4u * gd),
             "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
           : "memory");
-#if ENET_CRC_LANE0_ATOMICS
-      lds_add_nowait_l0(lds_addr(&S.consumed[slot]), 1u, l0, drow);
-#else
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
-#endif
     }
 #endif
-#endif
 #if ENET_CRC_RAGGED_PAIRS
-#if ENET_CRC_HDR_PACKED
     const uint32_t hw = __builtin_amdgcn_readfirstlane(hd.w);  // ns | B << 26 | fast << 31 (job build)
     const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
     const int32_t ns = rv ? (int32_t)(hw & 0x3FFFFFFu) : kPairMinSlots, B = rv ? (int32_t)((hw >> 26) & 15u) : 0;
     const bool fast = rv && (hw >> 31) != 0u;
     (void)n;
-#else
-    const int32_t mx = (int32_t)__builtin_amdgcn_readfirstlane(hd.x);
-    const uint32_t mn = __builtin_amdgcn_readfirstlane(hd.y);
-    const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
-    const int32_t ns = max(kPairMinSlots, (mx + 1) & ~1), B = ns - mx;
-    // fast: every valid packet's top slot ns - nsteps in B .. B + 1 (any in minimum rounds,
-    // empty packets included), no fallback chunk, an unrolled body for ns
-    // A round with positions past the batch (the batch's last round) is fast only when all its
-    // pairs come checked from the round before (ns = kPairMinSlots): an invalid position's
-    // record is ax = 0, and an unchecked pair would read at address 0 - 128 ns.
-    const int32_t lim = ns == kPairMinSlots ? kPairMinSlots : B + 1;
-    const bool partial = (d - k * RJ + 1u) * kPacketsPerWave > n;
-    const bool fast = !near_round && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)mn <= (int64_t)lim &&
-                      (!partial || ns == kPairMinSlots);
-#endif
     const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
-#if ENET_CRC_REC2
-    RaggedRound rr;
-    if (near_round) {
-      rr = pair_round_from_record2(ax, info, rv, c, ns, B, fast, true);
-      rr.plan = pair_plan2(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, true, c);
-    } else {
-      rr = pair_round_from_record2(ax, info, rv, c, ns, B, fast, false);
-      rr.plan = pair_plan2(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, false, c);
-    }
-#elif ENET_CRC_NEAR_SPLIT
     // Rounds holding a packet near the caller's base (the batch's first few) take their own copy
     // of the decode: the others carry no near-base code at all (one scalar branch).
     RaggedRound rr;
@@ -2856,11 +2499,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, false, c);
     }
 #else
-    RaggedRound rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u),
-                                            (uint32_t)(ax >> kJobLidShift) & 255u, c, ns, B, fast, near_round);
-    rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, near_round, c);
-#endif
-#else
     if (rv) {
       const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
       asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"  // one round trip
@@ -2873,11 +2511,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
     rr.live = live;
     rr.job_k = k;
-#if ENET_CRC_DIET
     rr.job_rounds = k + 1u == wg_jobs ? last_rounds : RJ;
-#else
-    rr.job_rounds = (n + kPacketsPerWave - 1) / kPacketsPerWave;
-#endif
     return rr;
   };
 
@@ -2897,23 +2531,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
     // The checksum store is not waited for on its own: the done counter's wait below covers
     // it (LDS operations complete in order).
-#if ENET_CRC_DIET
     {  // every lane stores: lane k == 0 of a valid packet into res[id], the others into res_dummy
       const uint32_t sel = (uint32_t)((int32_t)(meta << (31 - 10)) >> 31) &  // kMetaStore (bit 10)
                            (uint32_t)((int32_t)(c.k - 1u) >> 31);            // k == 0
       const uint32_t ra = lds_addr(&S.job[slot0].res[0]) + 4u * id, da = lds_addr(&S.res_dummy[0]) + 4u * lane;
       lds_st32_nowait((sel & ra) | (~sel & da), __builtin_bswap32(~reg));
     }
-#else
-    if (c.k == 0 && (meta & kMetaStore)) lds_st32_nowait(lds_addr(&S.job[slot0].res[id]), __builtin_bswap32(~reg));
-#endif
     uint32_t old = 0;
-#if ENET_CRC_LANE0_ATOMICS
-    old = lds_add_rtn_l0(lds_addr(&S.done[slot0]), 1u, l0, drow);
-#else
     if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
     old = __builtin_amdgcn_readfirstlane(old);
-#endif
     // After a failure in the workgroup nothing more is flushed: a job whose records or
     // result slot were skipped would leave stale checksums in res[].
     if (old + 1u == job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
@@ -2944,9 +2570,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   PairRing R;
   R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
   R.ring0 = lds_addr(&S.ring[0][wv][0]);
-#if ENET_CRC_DIET
   R.topmask = lds_addr(&S.topmask[0]);
-#endif
   {
     const uint32_t g = lane >> 3, k = lane & 7u, j = g & 3u;
     R.rd_a = 1024u * (g >> 2) + 256u * j + 128u * (j & 1u) + 16u * (7u - k);
@@ -2973,39 +2597,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #ifdef ENET_CRC_SPIN_STAMPS
   const uint64_t spin_t0 = __builtin_amdgcn_s_memtime();
 #endif
-#if ENET_CRC_TREE_ASM
   uint32_t tree_a = 0x10000u;  // tree_levels_asm's address register (high half 1, kept)
-#endif
-#if ENET_CRC_CLAIM_BATCH > 1
-  // Rounds are claimed kClaimBatch at a time (one LDS atomic per batch instead of per round).
-  // A batch's rounds are consecutive and taken in order, so a round is still claimed before
-  // every later one of this wave, and the claimer of a job's first round still reaches it
-  // before any round of the job it builds.
-  constexpr uint32_t kClaimBatch = ENET_CRC_CLAIM_BATCH;
-  uint32_t claim_next = 0, claim_left = 0;
-#endif
   while (cur.live) {  // cur is round rnd0
-#if ENET_CRC_CLAIM_BATCH > 1
-    if (claim_left == 0) {
-      uint32_t t = 0;
-      if (lane == 0) t = lds_add_rtn(lds_addr(&S.next_dispatch), kClaimBatch);
-      claim_next = __builtin_amdgcn_readfirstlane(t);
-      claim_left = kClaimBatch;
-    }
-    const uint32_t d = claim_next;
-    ++claim_next;
-    --claim_left;
-#elif defined(ENET_CRC_CLAIM_STATIC)  // measurement build: round d = rnd1 + 16, no atomics
-    const uint32_t d = rnd1 + (uint32_t)kWavesPerBlock;
-#else
-#if ENET_CRC_LANE0_ATOMICS
-    const uint32_t d = lds_add_rtn_l0(lds_addr(&S.next_dispatch), 1u, l0, drow);
-#else
     uint32_t d = 0;
     if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
     d = __builtin_amdgcn_readfirstlane(d);
-#endif
-#endif
     // Build duty: the claimer of a job's first round builds the job kJobAhead later (the
     // prologue built the first ones) once every round of the slot's previous job has read
     // its record.  That wait never closes a cycle: a round's record is read at the end of
@@ -3013,11 +2609,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // checksum slot below waits only for an older job's flush).
     bool build = false;
     const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
-#if ENET_CRC_DIET
     if (d == kd * RJ && kb >= first_jobs && kb < wg_jobs) {
-#else
-    if (d == kd * RJ && kb >= first_jobs && job_of(kb) < b.njobs) {
-#endif
       build = kb < (uint32_t)kJobSlots ||
               waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a SPIN_ACC(spin_consumed)), kFaultConsumed);
 #ifdef ENET_CRC_TEST_HOOKS
@@ -3053,14 +2645,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #endif
 #ifdef ENET_CRC_ABL_NOCOMBINE  // ablation build only (wrong checksums): the round end without its LDS trips
     uint32_t reg = h0 ^ h1 ^ h2 ^ h3;
-#elif ENET_CRC_TREE_ASM
+#else
     uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams
     y = apply_rep(lds, y, h2, c.lk.lp1, c.lk);
     y = apply_rep(lds, y, h3, c.lk.lp1, c.lk);
     y = tree_levels_asm(y, tree_a);
-    uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
-#else
-    const uint32_t y = combine_tree(lds, h0, h1, h2, h3, c.lk);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
 #endif
     if (cur.meta & kMetaEmpty) reg = kInitRegister;

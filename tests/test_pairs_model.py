@@ -231,7 +231,7 @@ def test_pair_ring_sequence():
 
 
 def test_pair_ring_sequence_staggered():
-    """The staggered refill (ENET_CRC_STAGGER, pair_step): the two DMAs of a refill pair go out
+    """The staggered refill (ENET_CRC_STAGGER, parked in profiles/r05/parked/): the two DMAs of a refill pair go out
     one compute slot apart (instruction 0 after half 0, instruction 1 after half 1, both into the
     pair slot just emptied).  Checked per DMA instruction across a wave's rounds, with the
     descriptor DMAs of a job build (3 per build) issued at random round starts: each compute
