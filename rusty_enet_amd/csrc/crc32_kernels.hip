@@ -772,9 +772,6 @@ struct UniformBatch {
 typedef __attribute__((address_space(3))) void LdsVoid;
 typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
-#ifndef ENET_CRC_RAGGED_PAIRS  // ragged jobs kernel: 256-B pair loads; 0: the round-4 loads (A/B builds)
-#define ENET_CRC_RAGGED_PAIRS 1
-#endif
 #ifndef ENET_CRC_RAGGED_RING
 #define ENET_CRC_RAGGED_RING 3  // A/B variants may build 4 (with ENET_CRC_JOB_SLOTS=4 for the LDS)
 #endif
@@ -1544,13 +1541,14 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
 }
 
 // ---------------------------------------------------------------------------------
-// Ragged rounds on the LDS-DMA ring (crc32_ragged_jobs_kernel below).  Packets come
+// Ragged rounds on the LDS-DMA pair ring (crc32_ragged_jobs_kernel below).  Packets come
 // sorted by step class, so the 8 packets of a round need (nearly) the same number of
-// slots; a round runs NS = max(kDmaRing, max steps of its 8) slots, and the packets with
-// fewer steps read the zero chunk in their leading slots.  Same ring and waits as
-// crc32_uniform_dma_kernel, with per-round, per-lane geometry from each packet's record
-// (round_from_record).  Trailing bytes as in the uniform DMA kernel: each packet runs to
-// the next 4-byte boundary with the bytes past its end masked, then finish_word.
+// slots; a round runs NS = max(kPairMinSlots, max steps of its 8 rounded up to even) compute
+// slots, loaded as NS / 2 pairs of 256 B per packet, and the packets with fewer steps read
+// the zero chunk in their leading slots.  Per-round, per-lane geometry comes from each
+// packet's record (round_from_record, pair_plan).  Trailing bytes as in the uniform DMA
+// kernel: each packet runs to the next 4-byte boundary with the bytes past its end masked,
+// then finish_word.
 // ---------------------------------------------------------------------------------
 // The DMA plan of one round for this lane: the address of its 16 B in pair 0 for each of its
 // two DMA packets (the packet's end minus 128 NS, plus the lane's offset inside the 256-B
@@ -1559,7 +1557,6 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
 // in the round's 128 NS-byte piece space minus the lane offset, the chunk of pair P is real
 // iff 256 P + 16 > t, i.e. P >= (t + 240) / 256.  An invalid or empty packet has t = 128 NS
 // minus the lane offset: never real.
-// (ENET_CRC_RAGGED_PAIRS builds only.)
 struct PairPlan {
   uint64_t db0, db1;
   int32_t p0, p1;  // first real pair of each DMA packet's chunk
@@ -1571,17 +1568,12 @@ struct RaggedRound {
   int32_t top_slot;     // slot of this lane's top chunk (ns: packet has no whole word)
   uint32_t meta;        // round_meta(); the trailing-byte field holds z (bytes run past the end)
   uint32_t id;          // packet id (output index)
-#if !ENET_CRC_RAGGED_PAIRS
-  uint32_t last_mask;   // lane 0: clears the bytes past the packet end in the last word
-#endif
   bool fast;            // wave-uniform: top slots in B .. B + 1 (any in ring-length rounds), no fallback, ns <= kRaggedFastMax
   bool live;            // jobs kernel: the round is inside the batch (wave-uniform)
   uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
   uint32_t job_rounds;  // jobs kernel: rounds of that job
   int32_t top_uniform;  // B: the first top slot of a fast round (0 unless ns == kRaggedRing)
-#if ENET_CRC_RAGGED_PAIRS
   PairPlan plan;        // this lane's DMA plan for the round
-#endif
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
@@ -1616,9 +1608,6 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
   rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
             (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
-#if !ENET_CRC_RAGGED_PAIRS
-  rr.last_mask = c.k == 0 ? 0xFFFFFFFFu >> (8u * z) : 0xFFFFFFFFu;
-#endif
   rr.id = id;
   // No packet of a fast round needs the fallback chunk (rule below).
   const bool fallback = __builtin_amdgcn_ballot_w64(rr.meta & kMetaFallback) != 0;
@@ -1633,119 +1622,7 @@ __device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t i
   return rr;
 }
 
-#if !ENET_CRC_RAGGED_PAIRS
-// Source of this lane's slot-s DMA in round rr (the zero chunk before its top).
-__device__ __forceinline__ uint64_t ragged_src(const RaggedRound& rr, int32_t s, uint64_t dummy) {
-  const bool real = s > rr.top_slot || (s == rr.top_slot && (rr.meta & kMetaDirect));
-  return real ? rr.cb + (uint64_t)kBytesPerStep * (uint64_t)s : dummy;
-}
 
-// Shared state of one wave's LDS-DMA ring (crc32_ragged_jobs_kernel).
-struct RaggedRing {
-  LdsVoid* slot0;     // this wave's ring position 0
-  uint32_t ring0;     // its LDS byte address
-  uint32_t lane16;    // lane * 16
-  uint32_t q;         // ring position of the slot being consumed (wave-uniform)
-  u32x4 nextv;        // landed data of the slot about to be consumed
-  __device__ __forceinline__ void dma(uint64_t src) {
-    __builtin_amdgcn_global_load_lds((const void*)src, (LdsVoid*)((LdsChar*)slot0 + q * kRingStride), 16, 0, 0);
-    q = q + 1 == (uint32_t)kRaggedRing ? 0u : q + 1;
-  }
-  __device__ __forceinline__ uint32_t next_addr() const { return ring0 + q * kRingStride + lane16; }
-};
-
-// A round whose packets' top slots lie in T .. T + 1 (T .. ring - 1 in ring-length rounds)
-// and that needs no fallback: the slot loop of crc32_uniform_dma_kernel (unrolled, lookups
-// fused with the next ring read); each lane masks its top words at its own top slot, lane
-// k == 0 the bytes past its packet's end in the last slot.  T > 0 only for rounds of packets
-// shorter than the ring (NS = kRaggedRing): their first T slots hold zero chunks and are only
-// consumed.
-template <int NS, int T = 0>
-__device__ __forceinline__ void ragged_round_fast(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
-                                                  const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                                  uint32_t& h3) {
-  static_assert(T == 0 || NS == kRaggedRing, "leading zero slots only in ring-length rounds");
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const u32x4 v = R.nextv;
-    const int32_t f = s + kRaggedRing;  // refill this slot's LDS slot kRaggedRing slots ahead
-    R.dma(f < NS ? cur.cb + (uint64_t)kBytesPerStep * (uint64_t)f : ragged_src(nxt, f - NS, c.dummy));
-    if (s < T) {
-      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
-      issue_order_fence();
-      continue;
-    }
-    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    if (s == NS - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
-    // each lane's own top slot (B .. B + 1, or B .. ring - 1 in ring-length rounds)
-    if (s <= (NS == kRaggedRing ? kRaggedRing - 1 : T + 1)) {
-      const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
-      if (__builtin_amdgcn_ballot_w64(mine)) {
-        if (mine) mask_top(cur.meta, w0, w1, w2, w3);
-      }
-    }
-    if (s == T) {
-      h0 = w0;  // first top slot B: every stream is still zero (M32^32(0) = 0), no lookups
-      h1 = w1;
-      h2 = w2;
-      h3 = w3;
-      R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
-    } else {
-      horner_step_and_read<kRaggedRing - 1>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, R.next_addr(), R.nextv);
-    }
-    issue_order_fence();
-  }
-}
-
-// Rounds of packets no longer than the ring (ns == kRaggedRing): top slot T = 0..ring-1.
-template <int... T>
-__device__ __forceinline__ bool ragged_round_short(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
-                                                   const LaneConsts& c, uint32_t& h0, uint32_t& h1, uint32_t& h2,
-                                                   uint32_t& h3, std::integer_sequence<int, T...>) {
-  return ((cur.top_uniform == T ? (ragged_round_fast<kRaggedRing, T>(cur, nxt, R, c, h0, h1, h2, h3), true) : false) ||
-          ...);
-}
-
-template <int... I>
-__device__ __forceinline__ bool ragged_round_dispatch(int32_t ns, const RaggedRound& cur, const RaggedRound& nxt,
-                                                      RaggedRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
-                                                      uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
-  if (ns == kRaggedRing) return ragged_round_short(cur, nxt, R, c, h0, h1, h2, h3,
-                                                   std::make_integer_sequence<int, kRaggedRing>{});
-  return ((ns == I + kRaggedRing + 1 ? (ragged_round_fast<I + kRaggedRing + 1>(cur, nxt, R, c, h0, h1, h2, h3), true)
-                                     : false) || ...);
-}
-
-// Any round (mixed step counts, fallback chunks, long packets): per-lane top slot.
-__device__ __forceinline__ void ragged_round_generic(const RaggedRound& cur, const RaggedRound& nxt, RaggedRing& R,
-                                                     const LaneConsts& c, const uint32_t* lds, uint32_t& h0,
-                                                     uint32_t& h1, uint32_t& h2, uint32_t& h3) {
-  for (int32_t s = 0; s < cur.ns; ++s) {
-    const u32x4 v = R.nextv;
-    const int32_t f = s + kRaggedRing;
-    R.dma(f < cur.ns ? ragged_src(cur, f, c.dummy) : ragged_src(nxt, f - cur.ns, c.dummy));
-    uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    const bool top = s == cur.top_slot;
-    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaFallback))) {
-      if (top && (cur.meta & kMetaFallback))
-        load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
-    }
-    if (s == cur.ns - 1) w3 &= cur.last_mask;  // data only: before the injection in mask_top
-    if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
-      if (top && (cur.meta & kMetaHeadMask)) mask_top(cur.meta, w0, w1, w2, w3);
-    }
-    h0 = horner_main(lds, h0, w0, c.lk);
-    h1 = horner_main(lds, h1, w1, c.lk);
-    h2 = horner_main(lds, h2, w2, c.lk);
-    h3 = horner_main(lds, h3, w3, c.lk);
-    R.nextv = read_landed_slot<kRaggedRing - 1>(R.next_addr());
-    issue_order_fence();
-  }
-}
-
-#endif  // !ENET_CRC_RAGGED_PAIRS
-
-#if ENET_CRC_RAGGED_PAIRS
 // ---------------------------------------------------------------------------------
 // Ragged rounds with 256-B loads.  The arithmetic and the compute
 // slots are those of the rounds above (8 lanes x 8 packets, 128 B of each packet per compute
@@ -2044,7 +1921,6 @@ __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const
     issue_order_fence();
   }
 }
-#endif  // ENET_CRC_RAGGED_PAIRS
 
 // ---------------------------------------------------------------------------------
 // Ragged kernel with in-kernel job sort (the default ragged path; no pre-pass, no
@@ -2071,7 +1947,7 @@ __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const
 constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
 constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
 #ifndef ENET_CRC_JOB_SLOTS
-#define ENET_CRC_JOB_SLOTS (ENET_CRC_RAGGED_PAIRS ? 4 : 6)  // pairs: the 64-KiB ring leaves room for 4
+#define ENET_CRC_JOB_SLOTS 4  // the 64-KiB pair ring leaves room for 4
 #endif
 constexpr int kJobSlots = ENET_CRC_JOB_SLOTS;                    // job slots in LDS
 constexpr int kJobAhead = 2;                                     // jobs built ahead of the one claimed
@@ -2090,21 +1966,15 @@ static_assert(kJobRecBytes == kJobPackets * 12, "staging: u64 offsets + u32 leng
 struct JobSlot {
   u32x4 rec[kJobRecBytes / 16];
   uint32_t res[kJobPackets];
-#if ENET_CRC_RAGGED_PAIRS
   // Per round of the job, from the job build: the largest and the smallest step count of its
   // valid packets, and bit 0 = one of them begins within 16 B of the caller's base (a top
   // chunk may need the fallback).  The round's slot count and its body follow from these
   // alone (no cross-lane reduction per round).
   u32x4 hdr[kJobRounds];
-#endif
 };
 struct RaggedJobsLds {
   uint32_t tables[kLdsDwords];
-#if ENET_CRC_RAGGED_PAIRS
   u32x4 ring[kPairRing][kWavesPerBlock][kPairBytes / 16];
-#else
-  u32x4 ring[kRaggedRing][kWavesPerBlock][64];
-#endif
   JobSlot job[kJobSlots];
   uint32_t ready[kJobSlots];     // k + 1 once the workgroup's k-th job has its records here
   uint32_t consumed[kJobSlots];  // rounds of the slot's job whose records have been read
@@ -2163,11 +2033,9 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(
 __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
-#if ENET_CRC_RAGGED_PAIRS
 __device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
-#endif
 
 #ifdef ENET_CRC_ROUND_STAMPS
 // Measurement build only (make variant NAME=stamps DEFS=-DENET_CRC_ROUND_STAMPS): per-wave
@@ -2291,7 +2159,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     LdsChar* st = (LdsChar*)&S.job[slot].rec[0];
     const uint64_t p0 = J * JP;
     if (p0 + kJobPackets <= b.count) {
-#if ENET_CRC_RAGGED_PAIRS
       // The lane's byte offset through an asm statement: hipcc would otherwise hoist the three
       // per-lane addresses out of the round loop and spill them (a scratch reload, then
       // vmcnt(0), at every job build).
@@ -2302,12 +2169,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       __builtin_amdgcn_global_load_lds((const void*)ob, (LdsVoid*)st, 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(ob + 1024), (LdsVoid*)(st + 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)lb, (LdsVoid*)(st + 2048), 16, 0, 0);
-#else
-      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 2 * lane), (LdsVoid*)st, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(b.offsets + p0 + 128 + 2 * lane), (LdsVoid*)(st + 1024), 16, 0,
-                                       0);
-      __builtin_amdgcn_global_load_lds((const void*)(b.lengths + p0 + 4 * lane), (LdsVoid*)(st + 2048), 16, 0, 0);
-#endif
     } else {
       // Not unrolled: one address live at a time (unrolled, hipcc hoisted all twelve out
       // of the round loop and spilled them to scratch: 18 MB of scratch writes per G2 launch).
@@ -2338,12 +2199,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                              o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
     const uint32_t len[4] = {ln.x, ln.y, ln.z, ln.w};
     const uint32_t n = job_count(J);
-#if ENET_CRC_RAGGED_PAIRS
     const uint32_t hdr = lds_addr(&S.job[slot].hdr[0]);
     if (lane < (uint32_t)kJobRounds) {  // max 0, min ~0, flags 0; in order before the atomics below
       asm volatile("ds_write_b128 %0, %1" : : "v"(hdr + 16u * lane), "v"(u32x4{0u, 0xFFFFFFFFu, 0u, 0u}) : "memory");
     }
-#endif
     uint64_t ax[4];
     uint32_t info[4], cls[4], rank[4];
 #pragma unroll
@@ -2351,11 +2210,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const bool v = 4u * lane + i < n;
       const RaggedRecord rec = ragged_record(b.base + off[i], len[i], c.base4);
       ax[i] = v ? rec.ax | ((uint64_t)(4u * lane + i) << kJobLidShift) : 0ull;
-#if ENET_CRC_RAGGED_PAIRS
       info[i] = v ? rec.info : 0u;  // an invalid position reads as an empty packet at address 0 (pair_plan)
-#else
-      info[i] = rec.info;
-#endif
       cls[i] = v ? (rec.nsteps < kStepClasses - 1 ? rec.nsteps : kStepClasses - 1) : (uint32_t)kStepClasses;
       rank[i] = 0;
 #pragma unroll
@@ -2390,15 +2245,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const uint32_t r = st + (q >> 3) * kJobRoundBytes;
       lds_st64(r + 8u * (q & 7u), ax[i]);
       lds_st32(r + 64u + 4u * (q & 7u), info[i]);
-#if ENET_CRC_RAGGED_PAIRS
       if (cls[i] < (uint32_t)kStepClasses) {  // a valid packet: the round header
         const uint32_t h = hdr + 16u * (q >> 3), ns_i = info[i] & kRecStepsMask;
         asm volatile("ds_max_u32 %0, %1\n\tds_min_u32 %0, %1 offset:4" : : "v"(h), "v"(ns_i) : "memory");
         if ((ax[i] >> kRecNearBit) & 1u) lds_or_nowait(h + 8u, 1u);
       }
-#endif
     }
-#if ENET_CRC_RAGGED_PAIRS
     // Per round, make_round's rule evaluated once here: hdr.w = ns | B << 26 | fast << 31 (the
     // header's max / min / near are complete: this wave's LDS atomics above are processed
     // before its read below).
@@ -2413,7 +2265,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                         (!partial || two_pairs);
       lds_st32(hdr + 16u * lane + 12u, (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u));
     }
-#endif
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
   };
 
@@ -2438,10 +2289,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #define SPIN_ACC(a)
 #endif
   const uint32_t fail_a = lds_addr(&S.failed);
-#if ENET_CRC_RAGGED_PAIRS
   // This lane's offset inside the 256-B pieces of its DMA packets (PairRing).
   const uint32_t dma_off = 128u * (((lane >> 3) ^ (lane >> 4)) & 1u) + 16u * (lane & 7u);
-#endif
   // A wait's outcome: true if the flag came; a wave's own time-out is reported.
   auto waited = [&](uint32_t w, uint32_t bit) -> bool {
     if (w == kWaitGaveUp) report_fault(fail_a, bit, b.fault);
@@ -2461,7 +2310,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #ifdef ENET_CRC_TEST_HOOKS
     if (rv && blockIdx.x == 0 && k + 1u == b.fault_k && b.fault_kind == kFaultReady) rv = waited(kWaitGaveUp, kFaultReady);
 #endif
-#if ENET_CRC_RAGGED_PAIRS
     u32x4 axd = {0, 0, 0, 0};  // the records of this lane's DMA packets lane / 16 and lane / 16 + 4
     uint64_t infod = 0;
     u32x4 hd = {0, 0, 0, 0};   // the round header: max steps, min steps, near flag
@@ -2478,8 +2326,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
           : "memory");
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
     }
-#endif
-#if ENET_CRC_RAGGED_PAIRS
     const uint32_t hw = __builtin_amdgcn_readfirstlane(hd.w);  // ns | B << 26 | fast << 31 (job build)
     const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
     const int32_t ns = rv ? (int32_t)(hw & 0x3FFFFFFu) : kPairMinSlots, B = rv ? (int32_t)((hw >> 26) & 15u) : 0;
@@ -2498,17 +2344,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                                   c, ns, B, fast, false);
       rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, false, c);
     }
-#else
-    if (rv) {
-      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
-      asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"  // one round trip
-                   : "=&v"(ax), "=&v"(info)
-                   : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp)
-                   : "memory");
-      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
-    }
-    RaggedRound rr = round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u, c);
-#endif
     rr.live = live;
     rr.job_k = k;
     rr.job_rounds = k + 1u == wg_jobs ? last_rounds : RJ;
@@ -2566,7 +2401,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   if (!round_valid(rnd0)) return;
   RaggedRound cur = make_round(rnd0);
   RaggedRound nxt = make_round(rnd1);
-#if ENET_CRC_RAGGED_PAIRS
   PairRing R;
   R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
   R.ring0 = lds_addr(&S.ring[0][wv][0]);
@@ -2580,16 +2414,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   R.issue(cur.plan, 0, 0, true, c);  // cur.ns >= kPairMinSlots: pairs 0 and 1
   R.issue(cur.plan, 1, 1, true, c);
   R.nextv = read_landed_slot<2>(R.addr_a(0));
-#else
-  RaggedRing R;
-  R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
-  R.ring0 = lds_addr(&S.ring[0][wv][0]);
-  R.lane16 = lane * 16u;
-  R.q = 0;
-#pragma unroll
-  for (int f = 0; f < kDmaRing; ++f) R.dma(ragged_src(cur, f, c.dummy));  // cur.ns >= kDmaRing
-  R.nextv = read_landed_slot<kDmaRing - 1>(R.next_addr());
-#endif
 #ifdef ENET_CRC_ROUND_STAMPS
   uint64_t st_body = 0, st_build = 0, st_rounds = 0, st_comb = 0, st_make = 0;
   const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
@@ -2629,15 +2453,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // rounds; no fallback chunk; NS <= kRaggedFastMax) take an unrolled body per NS, mixed-class
     // rounds included (round 4: 149.5 vs 157.8 us on G2); the others (fallback
     // chunks near the caller's base, longer or wider-spread rounds) the generic loop.
-#if ENET_CRC_RAGGED_PAIRS
     if (!cur.fast || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
                                           std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{}))
       pair_round_generic(cur, cur.plan, nxt.plan, R, c, lds, h0, h1, h2, h3);
-#else
-    if (!cur.fast || !ragged_round_dispatch(cur.ns, cur, nxt, R, c, h0, h1, h2, h3,
-                                            std::make_integer_sequence<int, kRaggedFastMax - kRaggedRing>{}))
-      ragged_round_generic(cur, nxt, R, c, lds, h0, h1, h2, h3);
-#endif
 #ifdef ENET_CRC_ROUND_STAMPS
     const uint64_t st_b1 = __builtin_amdgcn_s_memtime();
     st_body += st_b1 - st_b0;

@@ -1,4 +1,4 @@
-"""Host model of the ragged jobs kernel's 256-B pair loads (ENET_CRC_RAGGED_PAIRS,
+"""Host model of the ragged jobs kernel's 256-B pair loads (round 5,
 crc32_kernels.hip: PairRing, pair_plan, pair_step).  Restates the kernel's index arithmetic
 and checks, for random rounds of 8 packets (empty, invalid, near-base and long packets, odd
 and even step counts):
