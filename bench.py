@@ -527,6 +527,7 @@ def verify_batch(dev, batch: int = 256, reps: int = 200) -> dict:
 # --------------------------------------------------------------------------------------
 
 CEILING_LIB = os.path.join(REPO, "tools", "lib", "libenet_read_ceiling.so")
+CEILING_PRE_LAUNCHES = 40  # per read-ceiling variant before the main line's warmup (~30 ms of load)
 
 
 class ReadCeiling:
@@ -615,8 +616,9 @@ def ceiling_fields(ceil, pre: dict | None, data, nbytes: int, achieved_gbs: floa
                              "bytes": post["bytes"], "before_variants": pre["variants"],
                              "what": "tools/ceiling/read_ceiling.hip: the same device buffer read once with 16-B "
                                      "loads and an XOR, best of its variants measured before the warmup steps "
-                                     "(which also takes the GPU through its power-management transient, "
-                                     "DESIGN.md §6) and that variant again right after the timed steps "
+                                     f"({CEILING_PRE_LAUNCHES} launches each, ~30 ms of load, which also takes "
+                                     "the GPU through its clock transient, DESIGN.md §5) and that variant "
+                                     "again right after the timed steps "
                                      "(after_gbs = read_ceiling_gbs, 20 launches)"}}
 
 
@@ -839,9 +841,12 @@ def main(argv=None) -> int:
     if not args.no_verify:
         verify_sample(out, spec)
     # Same-buffer read ceiling, all variants, before the warmup steps (range: not bound by
-    # streaming reads, no ceiling).
+    # streaming reads, no ceiling).  40 timed launches per variant, ~30 ms of load in all: the
+    # shader clock drops within ~5 ms of load after an idle gap and climbs back over ~30 ms
+    # (profiles/r05/clock/), so the timed steps of any K start in the sustained
+    # state; the line's `cold` block times the same steps inside that window.
     ceil = None if is_range else open_ceiling(dev)
-    ceil_pre = ceil.measure(spec[1], nbytes) if ceil else None
+    ceil_pre = ceil.measure(spec[1], nbytes, launches=CEILING_PRE_LAUNCHES) if ceil else None
     for _ in range(args.warmup):
         step()
     wall, kernel_ms = time_steps(step, args.steps, barrier, dev)
