@@ -154,6 +154,29 @@ def test_full_size_ragged_1m(dev):
     assert np.array_equal(got, _oracle.crc32_ragged(d.cpu().numpy(), offsets, lengths))
 
 
+@pytest.mark.parametrize("layout", ["line_aligned", "packed_base_3"])
+def test_full_size_ragged_layouts(dev, layout):
+    """G2's 1M datagrams in the two other layouts round 5 measured: every datagram starting
+    on a 128-B line (scripts/exp_layout.py, the over-fetch A/B) and packed from
+    a buffer base 3 bytes past a line (every top chunk unaligned, the batch's first round near
+    the base); all checksums against the oracle (16 threads)."""
+    lengths = ragged_lengths(ENET_SEED, 1 << 20)
+    if layout == "line_aligned":
+        stride = (lengths.astype(np.uint64) + 127) // 128 * 128
+        offsets = np.concatenate([[0], np.cumsum(stride)[:-1]]).astype(np.uint64)
+    else:
+        offsets = packed_offsets(lengths) + np.uint64(3)
+    total = int(offsets[-1]) + int(lengths[-1])
+    g = torch.Generator(device=dev)
+    g.manual_seed(ENET_SEED + 21)
+    d = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    got = as_u32(rea.crc32_batch(d, offsets=to_dev(offsets.astype(np.int64), dev),
+                                 lengths=to_dev(lengths.astype(np.int32), dev)))
+    want = _oracle.crc32_ragged(d.cpu().numpy(), offsets, lengths, threads=16)
+    del d
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+
+
 def test_kernels_agree_on_the_same_bytes(dev):
     """HIP against HIP: the same packets through the uniform kernels (stride form) and the
     ragged jobs kernel (offsets / lengths form) give the same checksums, for G1's 1200-B
