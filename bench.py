@@ -855,7 +855,7 @@ def main(argv=None) -> int:
 
     # Cold: the same steps after an idle second, with only 5 launches of
     # warmup and no read-ceiling pass before them: the chip starts high, drops its shader clock
-    # after a few ms of load and climbs back over ~30 ms (DESIGN.md §6, profiles/r05/clock);
+    # after a few ms of load and climbs back over ~30 ms (DESIGN.md §5, profiles/r05/clock);
     # a bursty receive path sees this window.  Reported beside the line, never as its value.
     cold = None
     if not is_range and world == 1:

@@ -302,6 +302,9 @@ ENET_CRC_API uint32_t enet_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_
  * until enet_crc_ring_wait(ring, i) has returned, after which crcs[0..count) hold the
  * reference checksums.  Submitting a slot that is in flight is ENET_CRC_E_INVALID,
  * as is a packet outside the slot's bytes.  Calls on one ring are thread-safe.
+ * The status of a wait belongs to the slot's last submit: ENET_CRC_E_DEVICE as long as
+ * that submit's launch gave up on the device (every later wait on the slot says so too,
+ * until the next submit), else ENET_CRC_OK.
  */
 typedef struct enet_crc_ring enet_crc_ring;
 

@@ -198,44 +198,6 @@ __device__ __forceinline__ uint32_t head_k(uint32_t v) {
                 : (v == 1 ? kOpTables.head_k[1] : (v == 2 ? kOpTables.head_k[2] : kOpTables.head_k[3]));
 }
 
-#ifdef ENET_CRC_CLOCK_STAMPS
-// Measurement build only (make variant NAME=clock DEFS=-DENET_CRC_CLOCK_STAMPS;
-// scripts/exp_clock_series.py): the shader clock each launch of the whole-line and the
-// ragged jobs kernel ran at.  Every wave stores its (shader cycles, 100-MHz ticks) between
-// entry and exit into its own cell of the launch's row (the row is a kernel argument the
-// launcher counts on the host): plain stores, no atomics (a first version added every
-// wave's numbers into one word per launch; those same-address atomics at the end of each
-// launch made it 60-85 % slower).  Clock = sum cycles / sum ticks x 100 MHz over the row
-// (MI355X_MICROARCH.md "DVFS give-back" (6)).
-constexpr uint32_t kClockSlots = 512;
-constexpr uint32_t kClockWaves = 4096;  // 256 CUs x 16 waves
-__device__ unsigned long long g_clock_cells[kClockSlots][kClockWaves][2];
-std::atomic<uint32_t> g_clock_next{0};  // host: the next launch's row
-struct ClockStamp {
-  uint64_t t0, r0;
-  uint32_t row;
-  __device__ explicit ClockStamp(uint32_t launch_row) : row(launch_row) {
-    t0 = __builtin_amdgcn_s_memtime();
-    r0 = __builtin_amdgcn_s_memrealtime();
-    __builtin_amdgcn_s_waitcnt(0);
-  }
-  __device__ ~ClockStamp() {
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint32_t w = blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);
-    if ((threadIdx.x & 63u) != 0u || w >= kClockWaves || row >= kClockSlots) return;
-    g_clock_cells[row][w][0] = t1 - t0;
-    g_clock_cells[row][w][1] = r1 - r0;
-  }
-};
-#define ENET_CRC_CLOCK_STAMP(row) ClockStamp clock_stamp_(row)
-#define ENET_CRC_CLOCK_ROW uint32_t clock_row = 0;
-#else
-#define ENET_CRC_CLOCK_STAMP(row) (void)0
-#define ENET_CRC_CLOCK_ROW
-#endif
-
 __device__ __forceinline__ int32_t wave_max_over_groups(int32_t v) {
   int32_t m = __builtin_amdgcn_readlane(v, 0);
 #pragma unroll
@@ -743,7 +705,6 @@ struct UniformBatch {
   // (address and output), so one launch covers a head and a tail around a whole-line run.
   uint64_t skip_at = ~0ull;
   uint64_t skip = 0;
-  ENET_CRC_CLOCK_ROW  // measurement build only
 };
 
 // ---------------------------------------------------------------------------------
@@ -772,10 +733,6 @@ struct UniformBatch {
 typedef __attribute__((address_space(3))) void LdsVoid;
 typedef __attribute__((address_space(3))) char LdsChar;
 constexpr int kUniformRing = 5;                              // LDS slots per wave, uniform kernel
-#ifndef ENET_CRC_RAGGED_RING
-#define ENET_CRC_RAGGED_RING 3  // A/B variants may build 4 (with ENET_CRC_JOB_SLOTS=4 for the LDS)
-#endif
-constexpr int kRaggedRing = ENET_CRC_RAGGED_RING;            // ragged kernels (3 vs 4: same time)
 constexpr uint32_t kRingStride = kWavesPerBlock * 64 * 16;   // bytes between ring positions
 
 // All LDS of a DMA kernel in ONE variable, tables first: the fused asm lookups use
@@ -1428,7 +1385,6 @@ typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4;
 
 template <int NSL>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
-  ENET_CRC_CLOCK_STAMP(u.clock_row);
   send_servers_home();
   __shared__ __attribute__((aligned(16))) UniformRegsLds S;
   uint32_t* const lds = S.tables;
@@ -1488,26 +1444,15 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
         h2 = w2;
         h3 = w3;
       } else {
-#ifdef ENET_CRC_PROBE_G1_NOLOOKUPS  // measurement build only (wrong checksums): the loads alone
-        h0 ^= w0;
-        h1 ^= w1;
-        h2 ^= w2;
-        h3 ^= w3;
-#else
         h0 = horner_main(lds, h0, w0, c.lk);
         h1 = horner_main(lds, h1, w1, c.lk);
         h2 = horner_main(lds, h2, w2, c.lk);
         h3 = horner_main(lds, h3, w3, c.lk);
-#endif
       }
       issue_order_fence();
       q[s] = ld(lbn, s);  // the next round's slot s
       issue_order_fence();
     }
-#if defined(ENET_CRC_PROBE_G1_NOCOMBINE) || defined(ENET_CRC_PROBE_G1_NOLOOKUPS)
-    // Measurement builds only (wrong checksums): no handover, no combine.
-    const uint32_t reg = h0 ^ h1 ^ h2 ^ h3 ^ (uint32_t)kept.x;
-#else
     {
       const uint32_t a = ll.src4;
       const uint32_t x0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)a, (int)kept.x);
@@ -1523,7 +1468,6 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
     }
     const uint32_t y = combine_tree_rep(lds, h0, h1, h2, h3, c.lk);
     const uint32_t reg = finish_word(lds, y, 0u, c.lk);
-#endif
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
       res = crc;
@@ -1572,56 +1516,11 @@ struct RaggedRound {
   bool live;            // jobs kernel: the round is inside the batch (wave-uniform)
   uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
   uint32_t job_rounds;  // jobs kernel: rounds of that job
-  int32_t top_uniform;  // B: the first top slot of a fast round (0 unless ns == kRaggedRing)
+  int32_t top_uniform;  // B: the first top slot of a fast round (any of 0 .. 3 when ns == kPairMinSlots)
   PairPlan plan;        // this lane's DMA plan for the round
 };
 
-constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kRaggedRing .. kRaggedFastMax
-
-// Per-lane round state from the group's packet record (ragged_record's fields; an invalid
-// group -- past the batch, or a re-read record -- is an empty packet at base4).  Every
-// quantity is derived with 32-bit arithmetic from the precomputed geometry.
-// kMinSlots: the fewest slots a round runs (the ring's reach into the next round); kEven:
-// rounds run an even number of slots (the 256-B pair loads).
-template <int kMinSlots = kRaggedRing, bool kEven = false>
-__device__ __forceinline__ RaggedRound round_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t id,
-                                                         const LaneConsts& c) {
-  const uint64_t a1 = valid ? (ax & kRecAddrMask) : c.base4;
-  const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
-  const uint32_t pad = (info >> kRecPadShift) << 2;  // 128 nsteps - 4 nwords
-  const uint32_t v = valid ? (uint32_t)(ax >> kRecVShift) & 3u : 0u;
-  const uint32_t z = valid ? (uint32_t)(ax >> kRecZShift) & 3u : 0u;
-  RaggedRound rr;
-  const int32_t max_steps = wave_max_over_groups(nsteps);
-  rr.ns = max(kMinSlots, kEven ? (max_steps + 1) & ~1 : max_steps);
-  rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(rr.ns - 1);
-  rr.top_slot = rr.ns - nsteps;
-  // This lane's chunk at the top step, relative to top: chunk_offset(g, k, nsteps-1, top)
-  // = 4 nwords - 16 (k + 8 (nsteps - 1) + 1) = 112 - 16 k - pad.
-  const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
-  const bool inside = nsteps > 0 && rel > -16;  // not wholly before the packet
-  bool fb = false;                              // chunk_kind == kChunkFallback
-  if (((ax >> kRecNearBit) & 1u) && valid && inside && rel < 0) {
-    const uint64_t top = a1 - ((uint64_t)kBytesPerStep * (uint64_t)nsteps - pad);
-    fb = top - c.base4 < (uint64_t)(-rel);
-  }
-  const uint32_t head = inside && rel <= 0 ? (uint32_t)(rel / 4 + 4) : 0u;
-  rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
-            (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
-  rr.id = id;
-  // No packet of a fast round needs the fallback chunk (rule below).
-  const bool fallback = __builtin_amdgcn_ballot_w64(rr.meta & kMetaFallback) != 0;
-  // Fast (unrolled body): every top slot in B .. B + 1 (B = ns - max steps; B .. ring - 1 in
-  // ring-length rounds, empty packets included), so rounds where two step classes meet take
-  // the unrolled bodies too (27 % of G2's rounds; 149.5 vs 157.8 us).  All those
-  // slots were issued by the previous round with per-lane sources, every later slot lies
-  // inside every packet, and each lane masks its own top chunk at its top slot.
-  rr.top_uniform = rr.ns - max_steps;  // B
-  const int32_t lim = rr.ns == kMinSlots ? kMinSlots : rr.top_uniform + 1;
-  rr.fast = !__builtin_amdgcn_ballot_w64(rr.top_slot > lim) && !fallback && rr.ns <= kRaggedFastMax;
-  return rr;
-}
-
+constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kPairMinSlots .. kRaggedFastMax
 
 // ---------------------------------------------------------------------------------
 // Ragged rounds with 256-B loads.  The arithmetic and the compute
@@ -1774,13 +1673,8 @@ struct PairRing {
       s1 = P >= pl.p1 ? s1 : c.dummy;
     }
     LdsChar* const dst = (LdsChar*)slot0 + slot * kPairStride;
-#ifdef ENET_CRC_ABL_NODMA  // ablation build only (wrong checksums): the ring is never loaded
-    if (s0 == 0 && s1 == 1) __builtin_trap();  // keeps the address arithmetic
-    (void)dst;
-#else
     __builtin_amdgcn_global_load_lds((const void*)s0, (LdsVoid*)dst, 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 0);
-#endif
   }
   __device__ __forceinline__ uint32_t addr_a(uint32_t slot) const { return ring0 + slot * kPairStride + rd_a; }
   __device__ __forceinline__ uint32_t addr_b(uint32_t slot) const { return ring0 + slot * kPairStride + (rd_a ^ 128u); }
@@ -1799,26 +1693,12 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
                                           uint32_t w2, uint32_t w3) {
   const bool half0 = (s & 1) == 0;
   const uint32_t next_addr = half0 ? R.addr_b(R.q) : R.addr_a(R.q ^ 1u);
-#ifdef ENET_CRC_ABL_NOWAIT  // ablation builds only (wrong checksums): no wait for the ring's DMAs
-  constexpr int kWait = 63;
-#else
-  constexpr int kWait = 2;
-#endif
-#ifdef ENET_CRC_ABL_NOLOOKUP  // ablation: the slot's data XORed into the streams, no table lookups
-  if constexpr (kLook) {
-    h0 ^= w0;
-    h1 ^= w1;
-    h2 ^= w2;
-    h3 ^= w3;
-  }
-  R.nextv = read_landed_slot<kWait>(next_addr);
-#else
+  constexpr int kWait = 2;  // the two DMAs of the pair after the one read may stay in flight
   if constexpr (kLook) {
     horner_step_and_read<kWait>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
   } else {
     R.nextv = read_landed_slot<kWait>(next_addr);
   }
-#endif
   if (half0) {
     const int32_t f = s / 2 + kPairRing, np = ns / 2;  // the pair that refills pair slot R.q
     if (f < np)
@@ -1946,11 +1826,12 @@ __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const
 // ---------------------------------------------------------------------------------
 constexpr int kJobPackets = 256;                                 // 4 per lane of the building wave
 constexpr int kJobRounds = kJobPackets / kPacketsPerWave;        // 32
-#ifndef ENET_CRC_JOB_SLOTS
-#define ENET_CRC_JOB_SLOTS 4  // the 64-KiB pair ring leaves room for 4
-#endif
-constexpr int kJobSlots = ENET_CRC_JOB_SLOTS;                    // job slots in LDS
+constexpr int kMinJobRounds = kJobRounds / 2;                   // launch_ragged: RJ = 16 .. 32 rounds per job
+constexpr int kJobSlots = 4;                                     // job slots in LDS (the 64-KiB pair ring leaves room for 4)
 constexpr int kJobAhead = 2;                                     // jobs built ahead of the one claimed
+// The prologue builds every job the initial claims (rounds 0 .. 2 x 16 - 1) reach plus kJobAhead
+// more, each into a slot of its own.
+static_assert(kJobSlots >= (2 * kWavesPerBlock - 1) / kMinJobRounds + kJobAhead + 1, "prologue jobs need their slots");
 constexpr uint32_t kJobRoundBytes = 96;                          // per round: u64 ax[8], u32 info[8]
 constexpr uint32_t kJobRecBytes = kJobRounds * kJobRoundBytes;   // 3 KiB, also the descriptor staging
 constexpr int kJobLidShift = 54;                                 // local id (0..255) in ax bits 54..61
@@ -1995,7 +1876,6 @@ struct RaggedJobsBatch {
   uint64_t njobs;
   uint32_t job_packets;  // packets per job (<= kJobPackets), chosen so every workgroup gets the same job count
   uint32_t* fault;       // this launch's failure word (device address; launch_ragged: FaultWord)
-  ENET_CRC_CLOCK_ROW     // measurement build only
 #ifdef ENET_CRC_TEST_HOOKS
   // Test build: workgroup 0 gives up the fault_kind wait (kFaultReady / kFaultConsumed /
   // kFaultFreed) of its (fault_k - 1)-th job (fault_k == 0: none).
@@ -2037,49 +1917,12 @@ __device__ __forceinline__ void lds_or_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
-#ifdef ENET_CRC_ROUND_STAMPS
-// Measurement build only (make variant NAME=stamps DEFS=-DENET_CRC_ROUND_STAMPS): per-wave
-// s_memtime sums of the ragged jobs kernel, read back with enet_crc_debug_round_stamps:
-// [0] round bodies, [1] the whole round loop, [2] rounds, [3] job builds, [4] combine and
-// finish, [5] the next round's record read and plan (make_round).
-__device__ unsigned long long g_round_stamps[8];
-#endif
-
 // Spin (asleep) until the LDS word at `a` equals `want`.  kWaitOk, or kWaitGaveUp after
 // kJobSpinLimit polls, or kWaitFailFast as soon as the workgroup's failed word (at `fail`)
 // is set: one wave that gives up makes every later wait of its workgroup return at once,
 // so a broken pipeline drains in one pass instead of one time-out per round.
 enum : uint32_t { kWaitOk = 0, kWaitGaveUp = 1, kWaitFailFast = 2 };
-#ifdef ENET_CRC_SPIN_STAMPS
-// Measurement build only (make variant NAME=spin DEFS=-DENET_CRC_SPIN_STAMPS;
-// scripts/exp_spin.py): per wave of the last ragged jobs launch, the loop's shader cycles and,
-// per wait kind (ready, consumed, freed), how many waits found their flag unset and the cycles
-// they spun.  Plain stores of per-wave cells at the wave's end, no atomics.
-constexpr uint32_t kSpinWaves = 4096;
-__device__ unsigned long long g_spin_cells[kSpinWaves][8];
-struct SpinAcc {
-  unsigned long long n = 0, cyc = 0;
-};
-#endif
-__device__ __forceinline__ uint32_t lds_wait_eq(uint32_t a, uint32_t want, uint32_t fail
-#ifdef ENET_CRC_SPIN_STAMPS
-                                                , SpinAcc* acc = nullptr
-#endif
-) {
-#ifdef ENET_CRC_SPIN_STAMPS
-  if (acc && __builtin_amdgcn_readfirstlane(lds_ld32(a)) != want) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    uint32_t r = kWaitGaveUp;
-    for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
-      if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) { r = kWaitOk; break; }
-      if (__builtin_amdgcn_readfirstlane(lds_ld32(fail)) != 0u) { r = kWaitFailFast; break; }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    acc->n += 1;
-    acc->cyc += __builtin_amdgcn_s_memtime() - t0;
-    return r;
-  }
-#endif
+__device__ __forceinline__ uint32_t lds_wait_eq(uint32_t a, uint32_t want, uint32_t fail) {
   for (uint32_t i = 0; i < kJobSpinLimit; ++i) {
     if (__builtin_amdgcn_readfirstlane(lds_ld32(a)) == want) return kWaitOk;
     if (__builtin_amdgcn_readfirstlane(lds_ld32(fail)) != 0u) return kWaitFailFast;
@@ -2099,9 +1942,11 @@ __device__ __forceinline__ void report_fault(uint32_t fail, uint32_t bit, uint32
 }
 
 __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_jobs_kernel(RaggedJobsBatch b, uint32_t* __restrict__ out) {
-  ENET_CRC_CLOCK_STAMP(b.clock_row);
   send_servers_home();
-  constexpr int kDmaRing = kRaggedRing;
+  // job_build's wait for its descriptor DMAs: every round issues one ring DMA per compute slot
+  // (NS >= kPairMinSlots) after the job_dma of the iteration, so vmcnt(kDescWait) covers them.
+  constexpr int kDescWait = 2;
+  static_assert(kDescWait < kPairMinSlots, "a round issues >= kPairMinSlots DMAs after the descriptors'");
   __shared__ __attribute__((aligned(16))) RaggedJobsLds S;
   uint32_t* const lds = S.tables;
   constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
@@ -2184,14 +2029,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       }
     }
   };
-  // Phase B (>= kDmaRing DMAs after phase A): sort the job's packets by step class and
+  // Phase B (>= kPairMinSlots ring DMAs after phase A): sort the job's packets by step class and
   // write its round records in place of the descriptors; then mark the slot ready.
   auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
-#ifdef ENET_CRC_ABL_NODMA  // no ring DMAs are issued after the descriptors' (the wait below counts on them)
-    asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-#else
-    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDmaRing - 1) : "memory");
-#endif
+    asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDescWait) : "memory");
     const uint32_t st = lds_addr(&S.job[slot].rec[0]);
     const u32x4 o01 = lds_ld128(st + 32u * lane), o23 = lds_ld128(st + 32u * lane + 16u);
     const u32x4 ln = lds_ld128(st + 2048u + 16u * lane);
@@ -2281,13 +2122,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 
   // Jobs this wave has seen ready / flushed (a job's flags are polled once per wave).
   uint32_t seen_ready = 0, seen_freed = 0;
-#ifdef ENET_CRC_SPIN_STAMPS
-  SpinAcc spin_ready, spin_consumed, spin_freed;
-  uint64_t spin_rounds = 0;
-#define SPIN_ACC(a) , &a
-#else
-#define SPIN_ACC(a)
-#endif
   const uint32_t fail_a = lds_addr(&S.failed);
   // This lane's offset inside the 256-B pieces of its DMA packets (PairRing).
   const uint32_t dma_off = 128u * (((lane >> 3) ^ (lane >> 4)) & 1u) + 16u * (lane & 7u);
@@ -2304,7 +2138,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint32_t n = k + 1u == wg_jobs ? last_n : JP;
     bool rv = live;
     if (rv && k + 1u > seen_ready) {
-      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a SPIN_ACC(spin_ready)), kFaultReady);
+      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
       if (rv) seen_ready = k + 1u;
     }
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2357,7 +2191,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // writes the job's checksums to HBM.
     const uint32_t slot0 = k0 % kJobSlots;
     if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
-      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a SPIN_ACC(spin_freed)), kFaultFreed))
+      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
     }
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2414,13 +2248,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   R.issue(cur.plan, 0, 0, true, c);  // cur.ns >= kPairMinSlots: pairs 0 and 1
   R.issue(cur.plan, 1, 1, true, c);
   R.nextv = read_landed_slot<2>(R.addr_a(0));
-#ifdef ENET_CRC_ROUND_STAMPS
-  uint64_t st_body = 0, st_build = 0, st_rounds = 0, st_comb = 0, st_make = 0;
-  const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef ENET_CRC_SPIN_STAMPS
-  const uint64_t spin_t0 = __builtin_amdgcn_s_memtime();
-#endif
   uint32_t tree_a = 0x10000u;  // tree_levels_asm's address register (high half 1, kept)
   while (cur.live) {  // cur is round rnd0
     uint32_t d = 0;
@@ -2435,7 +2262,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
     if (d == kd * RJ && kb >= first_jobs && kb < wg_jobs) {
       build = kb < (uint32_t)kJobSlots ||
-              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a SPIN_ACC(spin_consumed)), kFaultConsumed);
+              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
 #ifdef ENET_CRC_TEST_HOOKS
       if (blockIdx.x == 0 && kb >= (uint32_t)kJobSlots && kb + 1u == b.fault_k && b.fault_kind == kFaultConsumed)
         build = waited(kWaitGaveUp, kFaultConsumed);
@@ -2446,9 +2273,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       }
     }
     uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-#ifdef ENET_CRC_ROUND_STAMPS
-    const uint64_t st_b0 = __builtin_amdgcn_s_memtime();
-#endif
     // Fast rounds (every valid packet's top in slots B .. B + 1, or anywhere in the shortest
     // rounds; no fallback chunk; NS <= kRaggedFastMax) take an unrolled body per NS, mixed-class
     // rounds included (round 4: 149.5 vs 157.8 us on G2); the others (fallback
@@ -2456,117 +2280,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     if (!cur.fast || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
                                           std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{}))
       pair_round_generic(cur, cur.plan, nxt.plan, R, c, lds, h0, h1, h2, h3);
-#ifdef ENET_CRC_ROUND_STAMPS
-    const uint64_t st_b1 = __builtin_amdgcn_s_memtime();
-    st_body += st_b1 - st_b0;
-    ++st_rounds;
-#endif
-#ifdef ENET_CRC_ABL_NOCOMBINE  // ablation build only (wrong checksums): the round end without its LDS trips
-    uint32_t reg = h0 ^ h1 ^ h2 ^ h3;
-#else
     uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams
     y = apply_rep(lds, y, h2, c.lk.lp1, c.lk);
     y = apply_rep(lds, y, h3, c.lk.lp1, c.lk);
     y = tree_levels_asm(y, tree_a);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
-#endif
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
-#ifdef ENET_CRC_ROUND_STAMPS
-    reg = __builtin_amdgcn_readfirstlane(reg) == 0x12345678u ? reg + 1u : reg;  // the combine ends here
-    st_comb += __builtin_amdgcn_s_memtime() - st_b1;
-#endif
     publish(cur.job_k, cur.id, cur.meta, cur.job_rounds, reg);
-#ifdef ENET_CRC_ABL_EXTRA_TRIPS  // measurement build: n more dependent LDS round trips per round
-    {
-      uint32_t x = lds_addr(&S.failed);
-#pragma unroll
-      for (int t = 0; t < ENET_CRC_ABL_EXTRA_TRIPS; ++t) {
-        uint32_t v;
-        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(x) : "memory");
-        x += v;  // S.failed == 0: the same address, a true dependency
-      }
-    }
-#endif
-#ifdef ENET_CRC_ABL_EXTRA_IVALU  // measurement build: n more VALU instructions per round, 8 independent chains
-    {
-      uint32_t x0 = reg, x1 = reg + 1u, x2 = reg + 2u, x3 = reg + 3u, x4 = reg + 4u, x5 = reg + 5u, x6 = reg + 6u,
-               x7 = reg + 7u;
-#pragma unroll
-      for (int t = 0; t < ENET_CRC_ABL_EXTRA_IVALU / 8; ++t)
-        asm volatile(
-            "v_xad_u32 %0, %0, %0, %0\n\tv_xad_u32 %1, %1, %1, %1\n\tv_xad_u32 %2, %2, %2, %2\n\t"
-            "v_xad_u32 %3, %3, %3, %3\n\tv_xad_u32 %4, %4, %4, %4\n\tv_xad_u32 %5, %5, %5, %5\n\t"
-            "v_xad_u32 %6, %6, %6, %6\n\tv_xad_u32 %7, %7, %7, %7"
-            : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7));
-      asm volatile("" : : "v"(x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7));
-    }
-#endif
-#ifdef ENET_CRC_ABL_EXTRA_SALU  // measurement build: n more SALU instructions per round, 4 independent chains
-    {
-      uint32_t y0 = rnd1, y1 = rnd1 + 1u, y2 = rnd1 + 2u, y3 = rnd1 + 3u;
-#pragma unroll
-      for (int t = 0; t < ENET_CRC_ABL_EXTRA_SALU / 4; ++t)
-        asm volatile("s_add_u32 %0, %0, 3\n\ts_add_u32 %1, %1, 5\n\ts_add_u32 %2, %2, 7\n\ts_add_u32 %3, %3, 9"
-                     : "+s"(y0), "+s"(y1), "+s"(y2), "+s"(y3) : : "scc");
-      asm volatile("" : : "s"(y0 ^ y1 ^ y2 ^ y3));
-    }
-#endif
-#ifdef ENET_CRC_ABL_EXTRA_VALU  // measurement build: n more dependent VALU instructions per round
-    {
-      uint32_t x = reg;
-#pragma unroll
-      for (int t = 0; t < ENET_CRC_ABL_EXTRA_VALU; ++t) asm volatile("v_xad_u32 %0, %0, %0, %0" : "+v"(x));
-      asm volatile("" : : "v"(x));
-    }
-#endif
-#ifdef ENET_CRC_ROUND_STAMPS
-    const uint64_t st_j0 = __builtin_amdgcn_s_memtime();
-#endif
     if (build) job_build(job_of(kb), bslot, kb + 1u);
-#ifdef ENET_CRC_ROUND_STAMPS
-    st_build += __builtin_amdgcn_s_memtime() - st_j0;
-#endif
-#ifdef ENET_CRC_ROUND_STAMPS
-    const uint64_t st_m0 = __builtin_amdgcn_s_memtime();
-#endif
     const RaggedRound after = make_round(d);
-#ifdef ENET_CRC_ROUND_STAMPS
-    st_make += __builtin_amdgcn_s_memtime() - st_m0 + (after.id == 0x7FFFFFFFu ? 1u : 0u);
-#endif
     rnd0 = rnd1;
     rnd1 = d;
     cur = nxt;
     nxt = after;
-#ifdef ENET_CRC_SPIN_STAMPS
-    ++spin_rounds;
-#endif
   }
-#ifdef ENET_CRC_SPIN_STAMPS
-  {
-    const uint64_t t1 = __builtin_amdgcn_s_memtime();
-    const uint32_t w = blockIdx.x * kWavesPerBlock + wv;
-    if (lane == 0 && w < kSpinWaves) {
-      g_spin_cells[w][0] = t1 - spin_t0;
-      g_spin_cells[w][1] = spin_rounds;
-      g_spin_cells[w][2] = spin_ready.n;
-      g_spin_cells[w][3] = spin_ready.cyc;
-      g_spin_cells[w][4] = spin_consumed.n;
-      g_spin_cells[w][5] = spin_consumed.cyc;
-      g_spin_cells[w][6] = spin_freed.n;
-      g_spin_cells[w][7] = spin_freed.cyc;
-    }
-  }
-#endif
-#ifdef ENET_CRC_ROUND_STAMPS
-  if (lane == 0) {
-    atomicAdd(&g_round_stamps[0], (unsigned long long)st_body);
-    atomicAdd(&g_round_stamps[1], (unsigned long long)(__builtin_amdgcn_s_memtime() - st_t0));
-    atomicAdd(&g_round_stamps[2], (unsigned long long)st_rounds);
-    atomicAdd(&g_round_stamps[3], (unsigned long long)st_build);
-    atomicAdd(&g_round_stamps[4], (unsigned long long)st_comb);
-    atomicAdd(&g_round_stamps[5], (unsigned long long)st_make);
-  }
-#endif
   __builtin_amdgcn_s_waitcnt(0);
 }
 
@@ -2643,9 +2370,6 @@ static hipError_t dispatch_uniform_regs(int ns, const UniformBatch& u, uint32_t*
 // gcd(L, 128) <= 8 steps): they go through the register ring, the whole-line kernel starts
 // at packet head.  False when no packet starts on a line (e.g. L = 1200 from base + 8).
 static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length, uint64_t& head) {
-#ifdef ENET_CRC_NO_LINES  // A/B build: the register ring for these batches too
-  return false;
-#endif
   if (stride != length || (length & 15u) != 0 || (base & 15u) != 0) return false;
   for (uint64_t h = 0; h < (uint64_t)kPacketsPerWave; ++h) {
     if (((base + h * length) & 127u) == 0) {
@@ -2659,9 +2383,6 @@ static bool lines_shape(uint64_t base, uint64_t stride, uint32_t length, uint64_
 template <int NSL>
 static hipError_t launch_uniform_lines(const UniformBatch& u0, uint32_t* out, hipStream_t stream, unsigned blocks) {
   UniformBatch u = u0;
-#ifdef ENET_CRC_CLOCK_STAMPS
-  u.clock_row = g_clock_next.fetch_add(1);
-#endif
   hipLaunchKernelGGL((crc32_uniform_lines_kernel<NSL>), dim3(blocks), dim3(kBlock), 0, stream, u, out);
   return hipGetLastError();
 }
@@ -2783,11 +2504,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   // so the launch lasts as long as the busiest workgroup's ceil(njobs / grid) jobs: the job
   // size (16..32 rounds) is the one that minimises that makespan in rounds (1M packets on
   // 256 CUs: 32 rounds of 16 packets, 8 jobs each).
-#ifndef ENET_CRC_MAX_JOB_ROUNDS  // A/B builds: shorter jobs (a job's rounds run closer together in time)
-#define ENET_CRC_MAX_JOB_ROUNDS kJobRounds
-#endif
-  constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = ENET_CRC_MAX_JOB_ROUNDS,
-                     kMinJobRounds = kJobRounds / 2;
+  constexpr uint64_t kRoundPackets = kPacketsPerWave, kMaxJobRounds = kJobRounds;
   const int cus = cu_count_for_current_device();
   if (cus <= 0) return hipErrorNoDevice;
   uint64_t jp = kMaxJobRounds * kRoundPackets, njobs = 0, best = ~0ull;
@@ -2840,9 +2557,6 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
   g_last_job_packets = jp;
   g_last_grid = jblocks;
 #endif
-#ifdef ENET_CRC_CLOCK_STAMPS
-  jb.clock_row = g_clock_next.fetch_add(1);
-#endif
   hipLaunchKernelGGL(crc32_ragged_jobs_kernel, dim3(jblocks), dim3(kBlock), 0, stream, jb, out);
   return hipGetLastError();
 }
@@ -2855,77 +2569,5 @@ extern "C" __attribute__((visibility("default"))) void enet_crc_debug_ragged_sha
   out[0] = enet_crc::g_last_njobs;
   out[1] = enet_crc::g_last_job_packets;
   out[2] = enet_crc::g_last_grid;
-}
-#endif
-
-#ifdef ENET_CRC_CLOCK_STAMPS
-// Measurement build only: out[2 i], out[2 i + 1] = launch row i's shader cycles and 100-MHz
-// ticks summed over its waves (i < n <= kClockSlots), *launches = rows handed out so far;
-// reset != 0 zeroes the rows and restarts the count.
-extern "C" __attribute__((visibility("default"))) int enet_crc_debug_clock_stamps(unsigned long long* out, int n,
-                                                                                  unsigned* launches, int reset) {
-  using enet_crc::kClockSlots;
-  using enet_crc::kClockWaves;
-  if (n < 0 || n > (int)kClockSlots) return -1;
-  if (hipDeviceSynchronize() != hipSuccess) return -3;
-  if (n > 0) {
-    std::vector<unsigned long long> rows((size_t)n * kClockWaves * 2);
-    if (hipMemcpyFromSymbol(rows.data(), HIP_SYMBOL(enet_crc::g_clock_cells), rows.size() * sizeof(rows[0])) !=
-        hipSuccess)
-      return -3;
-    for (int i = 0; i < n; ++i) {
-      unsigned long long c = 0, t = 0;
-      for (uint32_t w = 0; w < kClockWaves; ++w) {
-        c += rows[((size_t)i * kClockWaves + w) * 2];
-        t += rows[((size_t)i * kClockWaves + w) * 2 + 1];
-      }
-      out[2 * i] = c;
-      out[2 * i + 1] = t;
-    }
-  }
-  if (launches) *launches = enet_crc::g_clock_next.load();
-  if (reset) {
-    std::vector<unsigned long long> zero((size_t)kClockSlots * kClockWaves * 2, 0ull);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_clock_cells), zero.data(), zero.size() * sizeof(zero[0])) !=
-        hipSuccess)
-      return -3;
-    enet_crc::g_clock_next = 0;
-  }
-  return 0;
-}
-#endif
-
-#ifdef ENET_CRC_SPIN_STAMPS
-// Measurement build only: the per-wave cells of the last ragged jobs launch (8 words each, see
-// g_spin_cells), summed over the first `waves` waves into out[0..7]; reset != 0 zeroes them.
-extern "C" __attribute__((visibility("default"))) int enet_crc_debug_spin(unsigned long long* out, int waves, int reset) {
-  using enet_crc::kSpinWaves;
-  if (waves < 0 || waves > (int)kSpinWaves) return -1;
-  if (hipDeviceSynchronize() != hipSuccess) return -3;
-  std::vector<unsigned long long> cells((size_t)kSpinWaves * 8);
-  if (hipMemcpyFromSymbol(cells.data(), HIP_SYMBOL(enet_crc::g_spin_cells), cells.size() * sizeof(cells[0])) != hipSuccess)
-    return -3;
-  for (int j = 0; j < 8; ++j) out[j] = 0;
-  for (int w = 0; w < waves; ++w)
-    for (int j = 0; j < 8; ++j) out[j] += cells[(size_t)w * 8 + j];
-  if (reset) {
-    std::fill(cells.begin(), cells.end(), 0ull);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_spin_cells), cells.data(), cells.size() * sizeof(cells[0])) != hipSuccess)
-      return -3;
-  }
-  return 0;
-}
-#endif
-
-#ifdef ENET_CRC_ROUND_STAMPS
-// Measurement build only: g_round_stamps (see its definition); reset != 0 zeroes them.
-extern "C" __attribute__((visibility("default"))) int enet_crc_debug_round_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(enet_crc::g_round_stamps), sizeof(unsigned long long) * 8) != hipSuccess)
-    return -3;
-  if (reset) {
-    static const unsigned long long zero[8] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(enet_crc::g_round_stamps), zero, sizeof(zero)) != hipSuccess) return -3;
-  }
-  return 0;
 }
 #endif

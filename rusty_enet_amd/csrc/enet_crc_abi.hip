@@ -1069,7 +1069,9 @@ int enet_crc_ring_wait(enet_crc_ring* r, uint32_t slot) {
   RingSlot& s = r->slots[slot];
   {
     std::lock_guard<std::mutex> lk(r->lock);
-    if (!s.busy) return ENET_CRC_OK;
+    // Already waited for (or never submitted): the word still holds the last submit's outcome
+    // (cleared only by the next submit), so a second wait reports what the first did.
+    if (!s.busy) return faulted(s.fault) ? ENET_CRC_E_DEVICE : ENET_CRC_OK;
   }
   DeviceGuard g(r->device);
   const hipError_t e = hipEventSynchronize(s.done);

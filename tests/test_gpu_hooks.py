@@ -275,7 +275,7 @@ def test_ragged_failure_mid_batch(dev, kind):
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
         jobs, grid, jp = wg0_jobs()
-        assert len(jobs) >= 9, len(jobs)      # the consumed / freed waits start at job 6
+        assert len(jobs) >= 9, len(jobs)      # the consumed / freed waits start at job kJobSlots = 4
         k = len(jobs) - 3                     # a late job: earlier ones are flushed by then
         assert rea.device_status(0, clear=True) == 0
         os.environ["ENET_CRC_TEST_JOB_FAULT"] = "{kind}:%d" % (k + 1)
@@ -333,7 +333,8 @@ def test_ring_failure_belongs_to_its_slot(dev):
     """two ring slots in flight, only the second one's launch fails.  Each slot
     owns its failure word: waiting for the second returns ENET_CRC_E_DEVICE, waiting for the
     first (after it, so a shared word would already have been taken) returns OK with exact
-    checksums, the device word stays clear, and the failed slot is clean on its next submit."""
+    checksums, the device word stays clear, and the failed slot is clean on its next submit.
+    A repeated wait reports what the first one did."""
     run_hooked("""
         import os
         from rusty_enet_amd.ring import ReceiveRing
@@ -359,7 +360,10 @@ def test_ring_failure_belongs_to_its_slot(dev):
                 raise SystemExit("no E_DEVICE from the failed slot")
             except rea.CrcError as e:
                 assert e.status == _native.ENET_CRC_E_DEVICE, e.status
+            # ADVICE r5: a second wait on the failed slot reports the same outcome
+            assert _native.lib().enet_crc_ring_wait(ring._handle, 1) == _native.ENET_CRC_E_DEVICE
             ring.wait(0)                         # OK: the failure was not its own
+            assert _native.lib().enet_crc_ring_wait(ring._handle, 0) == _native.ENET_CRC_OK
             assert np.array_equal(ring.slot(0)[3][:n], want[0])
             assert rea.device_status(0) == 0
             ring.submit(1, n)
