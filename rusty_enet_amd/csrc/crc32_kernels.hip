@@ -1508,16 +1508,19 @@ struct PairPlan {
 
 struct RaggedRound {
   uint64_t cb;          // this lane's chunk address at slot 0
-  int32_t ns;           // slots of the round (wave-uniform)
   int32_t top_slot;     // slot of this lane's top chunk (ns: packet has no whole word)
   uint32_t meta;        // round_meta(); the trailing-byte field holds z (bytes run past the end)
   uint32_t id;          // packet id (output index)
-  bool fast;            // wave-uniform: top slots in B .. B + 1 (any in ring-length rounds), no fallback, ns <= kRaggedFastMax
-  bool live;            // jobs kernel: the round is inside the batch (wave-uniform)
-  uint32_t job_k;       // jobs kernel: the workgroup's job number of the round
-  uint32_t job_rounds;  // jobs kernel: rounds of that job
-  int32_t top_uniform;  // B: the first top slot of a fast round (any of 0 .. 3 when ns == kPairMinSlots)
+  // Wave-uniform, one SGPR each (the loop carries two rounds; every SGPR it carries is one the
+  // job build and the round bodies cannot use, and the kernel is at the 106-SGPR limit):
+  uint32_t hw;          // the round header's word (job build): ns | B << 26 | fast << 31
+  uint32_t d;           // the workgroup's round index (live, job number and job rounds follow from it)
   PairPlan plan;        // this lane's DMA plan for the round
+  __device__ int32_t ns() const { return (int32_t)(hw & 0x3FFFFFFu); }  // slots of the round
+  // B: the first top slot of a fast round (any of 0 .. 3 when ns == kPairMinSlots)
+  __device__ int32_t top_uniform() const { return (int32_t)((hw >> 26) & 15u); }
+  // top slots in B .. B + 1 (any in 4-slot rounds), no fallback, ns <= kRaggedFastMax
+  __device__ bool fast() const { return (int32_t)hw < 0; }
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kPairMinSlots .. kRaggedFastMax
@@ -1538,7 +1541,11 @@ constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kPairMinSl
 // flight.  The DMA lane decides per 16-B chunk whether it is real (at or after its packet's
 // top word, not below the caller's buffer) or the zero chunk.
 // ---------------------------------------------------------------------------------
-constexpr int kPairRing = 2;                                    // pair slots per wave
+#ifndef ENET_CRC_PAIR_RING
+#define ENET_CRC_PAIR_RING 2
+#endif
+constexpr int kPairRing = ENET_CRC_PAIR_RING;                   // pair slots per wave (1 or 2)
+static_assert(kPairRing == 1 || kPairRing == 2, "pair ring");
 // Lane k == 0 clears the z bytes past its packet's end in the last word (z in meta).
 __device__ __forceinline__ uint32_t last_word_mask(uint32_t meta, uint32_t k) {
   // No lane compare (hipcc hoists k == 0 into a lane mask, then spills it to a VGPR lane):
@@ -1590,7 +1597,8 @@ __device__ __forceinline__ void mask_top_lds(uint32_t meta, uint32_t table, uint
 }
 constexpr uint32_t kPairBytes = 2048;                           // one pair slot of one wave
 constexpr uint32_t kPairStride = kWavesPerBlock * kPairBytes;   // bytes between ring positions
-constexpr int kPairMinSlots = 2 * kPairRing;                    // a round's first 2 pairs come from the round before
+constexpr int kPairMinSlots = 4;                                // a round runs >= 2 pairs
+static_assert(kPairMinSlots >= 2 * kPairRing, "a round's first kPairRing pairs come from the round before");
 
 
 // From the two DMA packets' records (an invalid position reads as ax = info = 0: an empty
@@ -1623,15 +1631,15 @@ __device__ __forceinline__ PairPlan pair_plan(uint64_t ax0, uint32_t info0, uint
 // A pair round's per-lane state from its packet record and the round header (ns, B and
 // `fast` are wave-uniform, from the job build's per-round max / min step counts).
 __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint32_t info, bool valid, uint32_t id,
-                                                              const LaneConsts& c, int32_t ns, int32_t B, bool fast,
-                                                              bool near_round) {
+                                                              const LaneConsts& c, uint32_t hw, bool near_round) {
   const uint64_t a1 = ax & kRecAddrMask;
   const int32_t nsteps = valid ? (int32_t)(info & kRecStepsMask) : 0;
   const uint32_t pad = (info >> kRecPadShift) << 2;
   const uint32_t v = (uint32_t)(ax >> kRecVShift) & 3u;
   const uint32_t z = (uint32_t)(ax >> kRecZShift) & 3u;
   RaggedRound rr;
-  rr.ns = ns;
+  rr.hw = hw;
+  const int32_t ns = rr.ns();
   rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(ns - 1);
   rr.top_slot = ns - nsteps;
   const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
@@ -1647,8 +1655,6 @@ __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint3
   rr.meta = head | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
             (valid ? kMetaStore : 0u) | (fb ? kMetaFallback : 0u) | (inside && !fb ? kMetaDirect : 0u);
   rr.id = id;
-  rr.top_uniform = B;
-  rr.fast = fast;
   return rr;
 }
 
@@ -1692,8 +1698,8 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
                                           uint32_t& h1, uint32_t& h2, uint32_t& h3, uint32_t w0, uint32_t w1,
                                           uint32_t w2, uint32_t w3) {
   const bool half0 = (s & 1) == 0;
-  const uint32_t next_addr = half0 ? R.addr_b(R.q) : R.addr_a(R.q ^ 1u);
-  constexpr int kWait = 2;  // the two DMAs of the pair after the one read may stay in flight
+  const uint32_t next_addr = half0 ? R.addr_b(R.q) : R.addr_a(kPairRing == 2 ? R.q ^ 1u : R.q);
+  constexpr int kWait = 2 * (kPairRing - 1);  // the two DMAs of the pair after the one read may stay in flight
   if constexpr (kLook) {
     horner_step_and_read<kWait>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
   } else {
@@ -1701,12 +1707,14 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
   }
   if (half0) {
     const int32_t f = s / 2 + kPairRing, np = ns / 2;  // the pair that refills pair slot R.q
+    // Pairs 0 and 1 of a round may hold tops (fast rounds: slots B .. B + 1, B <= 1, or any of
+    // a 4-slot round's): issued checked, whoever issues them.
     if (f < np)
-      R.issue(cur, f, R.q, cur_checked, c);
+      R.issue(cur, f, R.q, cur_checked || f < kPairMinSlots / 2, c);
     else
       R.issue(nxt, f - np, R.q, true, c);
   } else {
-    R.q ^= 1u;
+    if (kPairRing == 2) R.q ^= 1u;
   }
 }
 
@@ -1752,7 +1760,7 @@ template <int... T>
 __device__ __forceinline__ bool pair_round_short(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
                                                  PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                  uint32_t& h2, uint32_t& h3, std::integer_sequence<int, T...>) {
-  return ((cur.top_uniform == T ? (pair_round_fast<kPairMinSlots, T>(cur, pc, pn, R, c, h0, h1, h2, h3), true)
+  return ((cur.top_uniform() == T ? (pair_round_fast<kPairMinSlots, T>(cur, pc, pn, R, c, h0, h1, h2, h3), true)
                                 : false) ||
           ...);
 }
@@ -1762,15 +1770,15 @@ template <int... I>
 __device__ __forceinline__ bool pair_round_dispatch(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
                                                     PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                     uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
-  if (cur.ns == kPairMinSlots)
+  if (cur.ns() == kPairMinSlots)
     return pair_round_short(cur, pc, pn, R, c, h0, h1, h2, h3, std::make_integer_sequence<int, kPairMinSlots>{});
-  if (cur.top_uniform == 0)
-    return ((cur.ns == kPairMinSlots + 2 * (I + 1)
+  if (cur.top_uniform() == 0)
+    return ((cur.ns() == kPairMinSlots + 2 * (I + 1)
                  ? (pair_round_fast<kPairMinSlots + 2 * (I + 1), 0>(cur, pc, pn, R, c, h0, h1, h2, h3), true)
                  : false) ||
             ...);
-  if (cur.top_uniform == 1)
-    return ((cur.ns == kPairMinSlots + 2 * (I + 1)
+  if (cur.top_uniform() == 1)
+    return ((cur.ns() == kPairMinSlots + 2 * (I + 1)
                  ? (pair_round_fast<kPairMinSlots + 2 * (I + 1), 1>(cur, pc, pn, R, c, h0, h1, h2, h3), true)
                  : false) ||
             ...);
@@ -1781,7 +1789,8 @@ __device__ __forceinline__ bool pair_round_dispatch(const RaggedRound& cur, cons
 __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
                                                    PairRing& R, const LaneConsts& c, const uint32_t* lds,
                                                    uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3) {
-  for (int32_t s = 0; s < cur.ns; ++s) {
+  const int32_t ns = cur.ns();
+  for (int32_t s = 0; s < ns; ++s) {
     const u32x4 v = R.nextv;
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     const bool top = s == cur.top_slot;
@@ -1789,7 +1798,7 @@ __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const
       if (top && (cur.meta & kMetaFallback))
         load_top_words(cur.cb + (uint64_t)kBytesPerStep * (uint64_t)s, cur.meta, c.dummy, w0, w1, w2, w3);
     }
-    if (s == cur.ns - 1) w3 &= last_word_mask(cur.meta, c.k);
+    if (s == ns - 1) w3 &= last_word_mask(cur.meta, c.k);
     if (__builtin_amdgcn_ballot_w64(top && (cur.meta & kMetaHeadMask))) {
       if (top && (cur.meta & kMetaHeadMask)) mask_top_lds(cur.meta, R.topmask, w0, w1, w2, w3);
     }
@@ -1797,7 +1806,7 @@ __device__ __forceinline__ void pair_round_generic(const RaggedRound& cur, const
     h1 = horner_main(lds, h1, w1, c.lk);
     h2 = horner_main(lds, h2, w2, c.lk);
     h3 = horner_main(lds, h3, w3, c.lk);
-    pair_step<false>(s, cur.ns, pc, pn, R, c, true, h0, h1, h2, h3, 0, 0, 0, 0);
+    pair_step<false>(s, ns, pc, pn, R, c, true, h0, h1, h2, h3, 0, 0, 0, 0);
     issue_order_fence();
   }
 }
@@ -1872,8 +1881,8 @@ struct RaggedJobsBatch {
   uint64_t base;
   const uint64_t* offsets;
   const uint32_t* lengths;
-  uint64_t count;
-  uint64_t njobs;
+  uint32_t count;        // < 2^32 (launch_ragged): the job arithmetic is 32-bit
+  uint32_t njobs;
   uint32_t job_packets;  // packets per job (<= kJobPackets), chosen so every workgroup gets the same job count
   uint32_t* fault;       // this launch's failure word (device address; launch_ragged: FaultWord)
 #ifdef ENET_CRC_TEST_HOOKS
@@ -1968,10 +1977,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
 
-  auto job_of = [&](uint32_t k) -> uint64_t { return (uint64_t)blockIdx.x + (uint64_t)k * gridDim.x; };
+  auto job_of = [&](uint32_t k) -> uint32_t { return blockIdx.x + k * gridDim.x; };  // < njobs, or >= it past the end
   const uint32_t JP = b.job_packets;
-  auto job_count = [&](uint64_t J) -> uint32_t {  // packets in job J (J < njobs)
-    const uint64_t left = b.count - J * JP;
+  auto job_count = [&](uint32_t J) -> uint32_t {  // packets in job J (J < njobs)
+    const uint64_t left = (uint64_t)b.count - (uint64_t)J * JP;
     return left < (uint64_t)JP ? (uint32_t)left : JP;
   };
   // Round d of this workgroup: round d % RJ of its (d / RJ)-th job, RJ = JP / 8 rounds
@@ -1985,13 +1994,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   auto div_rj = [&](uint32_t x) -> uint32_t { return __umulhi(x, rj_magic); };
   auto round_valid = [&](uint32_t d) -> bool {
     const uint32_t k = div_rj(d);
-    const uint64_t J = job_of(k);
-    return J < b.njobs && (uint64_t)(d - k * RJ) * kPacketsPerWave < job_count(J);
+    const uint32_t J = job_of(k);
+    return J < b.njobs && (d - k * RJ) * kPacketsPerWave < job_count(J);
   };
   // This workgroup's jobs k = 0 .. wg_jobs - 1 (job J = blockIdx.x + k grid); only its last can
   // hold fewer than JP packets.  Per round then: live = d < wg_rounds, and the job's packet and
   // round counts by one scalar compare (no 64-bit job arithmetic per round).
-  const uint32_t wg_jobs = (uint32_t)((b.njobs - blockIdx.x + gridDim.x - 1) / gridDim.x);
+  const uint32_t wg_jobs = (b.njobs - blockIdx.x + gridDim.x - 1) / gridDim.x;
   const uint32_t last_n = job_count(job_of(wg_jobs - 1u));
   const uint32_t last_rounds = (last_n + kPacketsPerWave - 1) / kPacketsPerWave;
   const uint32_t wg_rounds = (wg_jobs - 1u) * RJ + last_rounds;
@@ -2099,7 +2108,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const u32x4 hv = lds_ld128(hdr + 16u * lane);
       const int32_t mx = (int32_t)hv.x;
       const int32_t ns = max(kPairMinSlots, (mx + 1) & ~1), B = ns - mx;
-      const bool two_pairs = ns <= 2 * kPairRing;
+      const bool two_pairs = ns <= kPairMinSlots;  // every pair of the round is issued checked
       const int32_t lim = two_pairs ? ns : B + 1;
       const bool partial = (lane + 1u) * kPacketsPerWave > n;
       const bool fast = hv.z == 0u && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)hv.y <= (int64_t)lim &&
@@ -2134,9 +2143,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     uint64_t ax = 0;
     uint32_t info = 0;
     const uint32_t k = div_rj(d), slot = k % kJobSlots;
-    const bool live = d < wg_rounds;  // round_valid(d)
-    const uint32_t n = k + 1u == wg_jobs ? last_n : JP;
-    bool rv = live;
+    bool rv = d < wg_rounds;  // round_valid(d)
     if (rv && k + 1u > seen_ready) {
       rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
       if (rv) seen_ready = k + 1u;
@@ -2160,27 +2167,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
           : "memory");
       if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
     }
-    const uint32_t hw = __builtin_amdgcn_readfirstlane(hd.w);  // ns | B << 26 | fast << 31 (job build)
+    // ns | B << 26 | fast << 31 (job build); a round without records: 4 slots, B = 0, not fast
+    const uint32_t hw = rv ? __builtin_amdgcn_readfirstlane(hd.w) : (uint32_t)kPairMinSlots;
     const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
-    const int32_t ns = rv ? (int32_t)(hw & 0x3FFFFFFu) : kPairMinSlots, B = rv ? (int32_t)((hw >> 26) & 15u) : 0;
-    const bool fast = rv && (hw >> 31) != 0u;
-    (void)n;
+    const int32_t ns = (int32_t)(hw & 0x3FFFFFFu);
     const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
     // Rounds holding a packet near the caller's base (the batch's first few) take their own copy
     // of the decode: the others carry no near-base code at all (one scalar branch).
     RaggedRound rr;
     if (near_round) {
       rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u,
-                                  c, ns, B, fast, true);
+                                  c, hw, true);
       rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, true, c);
     } else {
       rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u,
-                                  c, ns, B, fast, false);
+                                  c, hw, false);
       rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, false, c);
     }
-    rr.live = live;
-    rr.job_k = k;
-    rr.job_rounds = k + 1u == wg_jobs ? last_rounds : RJ;
+    rr.d = d;
     return rr;
   };
 
@@ -2231,10 +2235,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       }
     }
   };
-  uint32_t rnd0 = wv, rnd1 = wv + kWavesPerBlock;
-  if (!round_valid(rnd0)) return;
-  RaggedRound cur = make_round(rnd0);
-  RaggedRound nxt = make_round(rnd1);
+  if (!round_valid(wv)) return;
+  RaggedRound cur = make_round(wv);
+  RaggedRound nxt = make_round(wv + kWavesPerBlock);
   PairRing R;
   R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
   R.ring0 = lds_addr(&S.ring[0][wv][0]);
@@ -2245,11 +2248,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     R.dma_off = dma_off;
   }
   R.q = 0;
-  R.issue(cur.plan, 0, 0, true, c);  // cur.ns >= kPairMinSlots: pairs 0 and 1
-  R.issue(cur.plan, 1, 1, true, c);
-  R.nextv = read_landed_slot<2>(R.addr_a(0));
+  for (int P = 0; P < kPairRing; ++P) R.issue(cur.plan, P, (uint32_t)P, true, c);  // cur.ns >= kPairMinSlots
+  R.nextv = read_landed_slot<2 * (kPairRing - 1)>(R.addr_a(0));
   uint32_t tree_a = 0x10000u;  // tree_levels_asm's address register (high half 1, kept)
-  while (cur.live) {  // cur is round rnd0
+  while (cur.d < wg_rounds) {  // the current round is inside the batch
     uint32_t d = 0;
     if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
     d = __builtin_amdgcn_readfirstlane(d);
@@ -2260,7 +2262,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // checksum slot below waits only for an older job's flush).
     bool build = false;
     const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
-    if (d == kd * RJ && kb >= first_jobs && kb < wg_jobs) {
+    if (d == kd * RJ && kb >= first_jobs && kb < wg_jobs) {  // rare: the first round of a job
       build = kb < (uint32_t)kJobSlots ||
               waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2277,7 +2279,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // rounds; no fallback chunk; NS <= kRaggedFastMax) take an unrolled body per NS, mixed-class
     // rounds included (round 4: 149.5 vs 157.8 us on G2); the others (fallback
     // chunks near the caller's base, longer or wider-spread rounds) the generic loop.
-    if (!cur.fast || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
+    if (!cur.fast() || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
                                           std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{}))
       pair_round_generic(cur, cur.plan, nxt.plan, R, c, lds, h0, h1, h2, h3);
     uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams
@@ -2286,11 +2288,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     y = tree_levels_asm(y, tree_a);
     uint32_t reg = finish_word(lds, y, (cur.meta >> kMetaNTailShift) & 3u, c.lk);  // lane k == 0 holds it
     if (cur.meta & kMetaEmpty) reg = kInitRegister;
-    publish(cur.job_k, cur.id, cur.meta, cur.job_rounds, reg);
+    {
+      const uint32_t k0 = div_rj(cur.d);
+      publish(k0, cur.id, cur.meta, k0 + 1u == wg_jobs ? last_rounds : RJ, reg);
+    }
     if (build) job_build(job_of(kb), bslot, kb + 1u);
     const RaggedRound after = make_round(d);
-    rnd0 = rnd1;
-    rnd1 = d;
     cur = nxt;
     nxt = after;
   }
@@ -2534,7 +2537,7 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     if ((err = hipGetDevice(&dev)) != hipSuccess || (err = device_fault_word(dev, &w)) != hipSuccess) return err;
     fault = w.dev;
   }
-  RaggedJobsBatch jb{b.base, offsets, lengths, count, njobs, (uint32_t)jp, fault};
+  RaggedJobsBatch jb{b.base, offsets, lengths, (uint32_t)count, (uint32_t)njobs, (uint32_t)jp, fault};
 #ifdef ENET_CRC_TEST_HOOKS
   // Test build only (tests/test_gpu_hooks.py): ENET_CRC_TEST_JOB_FAULT=<kind>:<k> makes
   // workgroup 0 give up its <kind> wait (ready, consumed, freed) for its (k-1)-th job; a

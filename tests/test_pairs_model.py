@@ -13,6 +13,7 @@ and even step counts):
   256-B bank row (no bank conflicts).
 """
 import numpy as np
+import pytest
 
 LANES, G, STEP = 64, 8, 128
 MIN_SLOTS = 4
@@ -177,37 +178,49 @@ def test_pair_loads_near_base():
     check(4, lambda r: r.integers(1, 300, size=8), trials=80)
 
 
-def test_pair_ring_sequence():
-    """The pair ring across a wave's rounds (pair_step restated): every compute slot reads the
-    (round, pair, half) it consumes from the pair slot that pair was loaded into, no pair slot
-    is refilled before its last read, and each vmcnt(2) wait leaves only the DMAs of the most
-    recently issued pair in flight, never the one being read (DMAs complete in issue order)."""
-    rng = np.random.default_rng(7)
+@pytest.mark.parametrize("ring", [1, 2])
+def test_pair_ring_sequence(ring):
+    """The pair ring across a wave's rounds (pair_step restated, kPairRing = `ring` pair
+    slots): every compute slot reads the (round, pair, half) it consumes from the pair slot
+    that pair was loaded into, no pair slot is refilled before its last read, and each
+    vmcnt(2 (ring - 1)) wait leaves only the DMAs of pairs issued after the one being read in
+    flight (DMAs complete in issue order).  A job build's descriptor DMAs (3 per build) go out
+    at random round starts; its own wait, vmcnt(kDescWait = 2) at the end of the round, must
+    find them landed.  Pairs 0 and 1 of every round are issued checked: by the round before
+    (P < ring) or by the round itself (ring 1: pair 1)."""
+    rng = np.random.default_rng(7 + ring)
     for _ in range(200):
         rounds = [2 * int(x) for x in rng.integers(2, 8, size=int(rng.integers(1, 12)))] + [4]  # + a trailing round
         slot_of = {}  # (round, pair) -> LDS pair slot
         dmas = []     # issue order of (round, pair) (2 DMA instructions each)
         reads_left = {}
 
-        def issue(r, P, q):
+        checked = {}  # (round, pair) -> issued checked
+
+        def issue(r, P, q, chk):
             assert all(v == 0 for (rr, pp), v in reads_left.items() if slot_of.get((rr, pp)) == q), \
                 ("refilled before its last read", r, P, q)
             assert P < rounds[r] // 2
             slot_of[(r, P)] = q
             reads_left[(r, P)] = 2
-            dmas.append((r, P))
+            checked[(r, P)] = chk
+            dmas.extend([("ring", r, P)] * 2)  # two DMA instructions per pair
 
-        def landed():  # after vmcnt(2): all but the last 2 DMA instructions (the last pair)
-            return dmas[:-1]
+        def landed(n):  # after vmcnt(n): all but the last n DMA instructions
+            return set(dmas[:len(dmas) - n])
 
-        # prologue: pairs 0 and 1 of round 0 into pair slots 0 and 1, then read compute slot 0
-        issue(0, 0, 0)
-        issue(0, 1, 1)
-        assert (0, 0) in landed()
+        wait = 2 * (ring - 1)
+        # prologue: pairs 0 .. ring - 1 of round 0 into pair slots 0 .. ring - 1, then read compute slot 0
+        for P in range(ring):
+            issue(0, P, P, True)
+        assert ("ring", 0, 0) in landed(wait)
         reads_left[(0, 0)] -= 1
         nextv, q = (0, 0, 0), 0
         for r in range(len(rounds) - 1):
             ns = rounds[r]
+            job = rng.random() < 0.3
+            if job:  # job_dma at the start of the iteration
+                dmas.extend([("job", r)] * 3)
             for s in range(ns):
                 P, half = s >> 1, s & 1
                 assert nextv == (r, P, half), (nextv, r, P, half)
@@ -216,18 +229,22 @@ def test_pair_ring_sequence():
                     assert slot_of[(r, P)] == q
                 else:
                     nxt = (r + 1, 0, 0) if s == ns - 1 else (r, P + 1, 0)
-                    assert slot_of[(nxt[0], nxt[1])] == q ^ 1, (nxt, q)
-                    assert (nxt[0], nxt[1]) in landed(), ("not landed at vmcnt(2)", nxt, dmas[-3:])
+                    assert slot_of[(nxt[0], nxt[1])] == (q + 1) % ring, (nxt, q)
+                    assert ("ring", nxt[0], nxt[1]) in landed(wait), ("not landed", nxt, dmas[-3:])
                 reads_left[(nxt[0], nxt[1])] -= 1
                 nextv = nxt
-                if half == 0:  # pair slot q's last half has been read: refill it with pair P + 2
-                    f = P + 2
+                if half == 0:  # pair slot q's last half has been read: refill it with pair P + ring
+                    f = P + ring
                     if f < ns // 2:
-                        issue(r, f, q)
+                        issue(r, f, q, f < 2)  # fast rounds: own pairs unchecked from pair 2 on
                     else:
-                        issue(r + 1, f - ns // 2, q)
+                        issue(r + 1, f - ns // 2, q, True)
                 else:
-                    q ^= 1
+                    q = (q + 1) % ring
+            if job:  # job_build after the round: vmcnt(kDescWait = 2)
+                assert ("job", r) in landed(2), ("descriptors not landed", dmas[-6:])
+        for (r, P), chk in checked.items():
+            assert P >= 2 or chk, ("a round's pair 0 / 1 went out unchecked", r, P)
 
 
 def test_pair_ring_sequence_staggered():
