@@ -266,6 +266,9 @@ constexpr uint32_t kMetaTShiftShift = 8;      // 2 bits: first trailing byte's p
 constexpr uint32_t kMetaStore = 1u << 10;     // packet index < count
 constexpr uint32_t kMetaFallback = 1u << 11;  // top chunk begins before the caller's buffer
 constexpr uint32_t kMetaDirect = 1u << 12;    // ragged rounds: the top chunk is read directly (inside, no fallback)
+constexpr uint32_t kMetaLineRShift = 13;      // line rounds: 2 bits, r = (E16 - a1) / 4 words
+constexpr uint32_t kMetaSkipShift = 15;       // line rounds: 4 bits, words not multiplied in at the last slot
+constexpr uint32_t kHeadZero = 5;             // line rounds: head code of a chunk wholly before the first word
 
 __device__ __forceinline__ uint32_t round_meta(const PacketGeo& g, uint32_t k, uint64_t base4, bool store,
                                                uint64_t& tail_addr, uint64_t dummy) {
@@ -1513,7 +1516,7 @@ struct RaggedRound {
   uint32_t id;          // packet id (output index)
   // Wave-uniform, one SGPR each (the loop carries two rounds; every SGPR it carries is one the
   // job build and the round bodies cannot use, and the kernel is at the 106-SGPR limit):
-  uint32_t hw;          // the round header's word (job build): ns | B << 26 | fast << 31
+  uint32_t hw;          // the round header's word (job build): ns | B << 26 | line << 30 | fast << 31
   uint32_t d;           // the workgroup's round index (live, job number and job rounds follow from it)
   PairPlan plan;        // this lane's DMA plan for the round
   __device__ int32_t ns() const { return (int32_t)(hw & 0x3FFFFFFu); }  // slots of the round
@@ -1521,9 +1524,23 @@ struct RaggedRound {
   __device__ int32_t top_uniform() const { return (int32_t)((hw >> 26) & 15u); }
   // top slots in B .. B + 1 (any in 4-slot rounds), no fallback, ns <= kRaggedFastMax
   __device__ bool fast() const { return (int32_t)hw < 0; }
+  // a line round (line_round_from_record): whole-line slots, always fast
+  __device__ bool line() const { return ((hw >> 30) & 1u) != 0u; }
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kPairMinSlots .. kRaggedFastMax
+#ifndef ENET_CRC_LINE_ROUNDS
+#define ENET_CRC_LINE_ROUNDS 1
+#endif
+constexpr bool kLineRounds = ENET_CRC_LINE_ROUNDS != 0;  // line_round_from_record (0: A/B builds)
+#ifndef ENET_CRC_LINE_MIN_STEPS
+#define ENET_CRC_LINE_MIN_STEPS 8
+#endif
+#ifndef ENET_CRC_LINE_NT
+#define ENET_CRC_LINE_NT 1
+#endif
+constexpr int kLineMinSteps = ENET_CRC_LINE_MIN_STEPS;    // the shortest packets a line round holds
+constexpr bool kLineNT = ENET_CRC_LINE_NT != 0;           // interior pairs of line rounds non-temporal
 
 // ---------------------------------------------------------------------------------
 // Ragged rounds with 256-B loads.  The arithmetic and the compute
@@ -1572,6 +1589,8 @@ __device__ __forceinline__ void fill_top_masks(TopMaskEntry* t) {
       m[i] = i < j0 ? 0u : (i == j0 ? 0xFFFFFFFFu << (8u * v) : 0xFFFFFFFFu);
       x[i] = i == j0 ? head_k(v) : 0u;
     }
+  } else if (head == kHeadZero) {  // line rounds: a chunk of the first line before the packet
+    m[0] = m[1] = m[2] = m[3] = 0u;
   }
   t[e].m = u32x4{m[0], m[1], m[2], m[3]};
   t[e].x = u32x4{x[0], x[1], x[2], x[3]};
@@ -1659,6 +1678,92 @@ __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint3
 }
 
 
+// ---------------------------------------------------------------------------------
+// Line rounds (round 6; host model: tests/test_line_rounds_model.py).  A round of 8 packets
+// of one step count n in 8 .. 13 (no partial round, no packet near the caller's base) may run
+// on whole 128-B lines instead of 128-B pieces ending at each packet's a1: compute slot s of
+// packet g is the line NS - 1 - s lines before the packet's last line; a packet of n steps
+// spans n or n + 1 lines, NS = the round's largest line count rounded up to even (the job build
+// ORs a header bit for a packet of n + 1 lines), so every first line is slot B or B + 1.  Every DMA then reads whole lines, and the pairs that hold no line a
+// neighbour shares (pairs 2 .. NS / 2 - 2) carry the non-temporal hint: tools/lines_probe,
+// 1392-B packets 225.2 vs 254.5 us.  The arithmetic stays the 8-lane Horner on
+// the 16-B grid ending at E16 = a1 rounded up to 16:
+//   * lane k holds the chunks c = k mod 8 counted back from E16: chunk (j_last - k) mod 8 of
+//     every line, j_last = the E16 chunk's index in the last line.  The DMA lane that fills
+//     LDS position p (read by compute lane 7 - p) loads chunk (p + j_last + 1) mod 8;
+//   * at the last slot the chunks past E16 (lanes k > j_last) and lane 0's words past a1 are
+//     not multiplied in (the meta's skip mask): those streams keep their previous value;
+//   * r = (E16 - a1) / 4: before the in-lane Horner, lane k forms the a1-grid chunk of its
+//     class from its own words 0 .. 3 - r and lane (k + 1) mod 8's words 4 - r .. 3
+//     (line_rotate; lane 7 takes lane 0's skipped words, one stream step behind);
+//   * at its first line each lane masks its chunk from the mask table: before the first
+//     word (kHeadZero), the first word's chunk (head, v: the init register injected), or none.
+// Line and chunk indices use the addresses' low 32 bits (a packet spans < 2^25 lines).
+__device__ __forceinline__ RaggedRound line_round_from_record(uint64_t ax, uint32_t info, uint32_t id,
+                                                              const LaneConsts& c, uint32_t hw) {
+  const uint32_t a1l = (uint32_t)ax;
+  const uint32_t nsteps = info & kRecStepsMask, pad = (info >> kRecPadShift) << 2;
+  const uint32_t topl = a1l - (128u * nsteps - pad);
+  const uint32_t lines = ((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) + 1u;
+  RaggedRound rr;
+  rr.hw = hw;
+  rr.cb = 0;  // no fallback chunks in a line round
+  rr.top_slot = rr.ns() - (int32_t)lines;
+  const uint32_t j_last = ((a1l - 1u) >> 4) & 7u, r = ((0u - a1l) >> 2) & 3u;
+  const uint32_t jk = (j_last - c.k) & 7u, jt = (topl >> 4) & 7u, wt = (topl >> 2) & 3u;
+  const uint32_t head = jk < jt ? kHeadZero : (jk == jt ? 4u - wt : 0u);
+  const uint32_t skip = c.k > j_last ? 0xFu : (c.k == 0u ? (0xF0u >> r) & 0xFu : 0u);
+  const uint32_t v = (uint32_t)(ax >> kRecVShift) & 3u, z = (uint32_t)(ax >> kRecZShift) & 3u;
+  rr.meta = head | (v << kMetaVShift) | (z << kMetaNTailShift) | kMetaStore | (r << kMetaLineRShift) |
+            (skip << kMetaSkipShift);
+  rr.id = id;
+  return rr;
+}
+
+// The DMA plan of a line round: for each DMA packet, the lane's 16 B of pair 0 (half h of the
+// pair: the line NS - 1 - h lines before the last one; chunk (p + j_last + 1) mod 8 of it) and
+// the first pair whose line of half h is one of the packet's (earlier ones: the zero chunk).
+__device__ __forceinline__ PairPlan line_pair_plan(uint64_t ax0, uint32_t info0, uint64_t ax1, uint32_t info1,
+                                                   int32_t ns, uint32_t lane) {
+  const uint32_t h = ((lane >> 3) ^ (lane >> 4)) & 1u, p = lane & 7u;
+  auto one = [&](uint64_t ax, uint32_t info, uint64_t& db) -> int32_t {
+    const uint64_t a1 = ax & kRecAddrMask;
+    const uint32_t a1l = (uint32_t)a1, nsteps = info & kRecStepsMask, pad = (info >> kRecPadShift) << 2;
+    const uint32_t topl = a1l - (128u * nsteps - pad);
+    const int32_t lines = (int32_t)((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) + 1;
+    db = ((a1 - 1u) & ~127ull) - 128u * (uint64_t)(ns - 1 - (int32_t)h) + 16u * ((p + ((a1l - 1u) >> 4) + 1u) & 7u);
+    const int32_t x = ns - lines - (int32_t)h;  // slot of the first line, minus h
+    return x > 0 ? (x + 1) >> 1 : 0;
+  };
+  PairPlan pl;
+  pl.p0 = one(ax0, info0, pl.db0);
+  pl.p1 = one(ax1, info1, pl.db1);
+  return pl;
+}
+
+// Before the in-lane Horner of a line round: the streams of this lane's a1-grid class,
+// g_i = own word i - r for i >= r, else word i - r + 4 of lane (k + 1) mod 8 (ds_bpermute, in
+// an asm statement with its own wait: hipcc would put a plain LDS access behind the ring DMAs).
+__device__ __forceinline__ void line_rotate(uint32_t meta, uint32_t lane, uint32_t& h0, uint32_t& h1, uint32_t& h2,
+                                            uint32_t& h3) {
+  const uint32_t src = 4u * ((lane & ~7u) | ((lane + 1u) & 7u));
+  uint32_t n1, n2, n3;
+  asm volatile(
+      "ds_bpermute_b32 %0, %3, %4\n\tds_bpermute_b32 %1, %3, %5\n\tds_bpermute_b32 %2, %3, %6\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(n1), "=&v"(n2), "=&v"(n3)
+      : "v"(src), "v"(h1), "v"(h2), "v"(h3));
+  const uint32_t r = (meta >> kMetaLineRShift) & 3u;
+  const uint32_t g0 = r == 0u ? h0 : (r == 1u ? n3 : (r == 2u ? n2 : n1));
+  const uint32_t g1 = r == 0u ? h1 : (r == 1u ? h0 : (r == 2u ? n3 : n2));
+  const uint32_t g2 = r == 0u ? h2 : (r == 1u ? h1 : (r == 2u ? h0 : n3));
+  const uint32_t g3 = r == 0u ? h3 : (r == 1u ? h2 : (r == 2u ? h1 : h0));
+  h0 = g0;
+  h1 = g1;
+  h2 = g2;
+  h3 = g3;
+}
+
 // Per-lane constants of the pair ring.
 struct PairRing {
   uint32_t topmask;  // LDS address of the top-chunk mask table (mask_top_lds)
@@ -1669,9 +1774,10 @@ struct PairRing {
   uint32_t q;        // pair slot of the pair being consumed (wave-uniform, 0 / 1)
   u32x4 nextv;       // landed data of the compute slot about to be consumed
   // Both DMAs of pair P of a round with plan pl into pair slot `slot`; `checked`: some chunk
-  // of this pair may lie before its packet's top (or below the caller's buffer).
+  // of this pair may lie before its packet's top (or below the caller's buffer); `nt`: the
+  // non-temporal hint (a line round's interior pairs; a compile-time constant where true).
   __device__ __forceinline__ void issue(const PairPlan& pl, int32_t P, uint32_t slot, bool checked,
-                                        const LaneConsts& c) {
+                                        const LaneConsts& c, bool nt = false) {
     const uint64_t o = 256u * (uint64_t)P;
     uint64_t s0 = pl.db0 + o, s1 = pl.db1 + o;
     if (checked) {
@@ -1679,8 +1785,13 @@ struct PairRing {
       s1 = P >= pl.p1 ? s1 : c.dummy;
     }
     LdsChar* const dst = (LdsChar*)slot0 + slot * kPairStride;
-    __builtin_amdgcn_global_load_lds((const void*)s0, (LdsVoid*)dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 0);
+    if (nt) {
+      __builtin_amdgcn_global_load_lds((const void*)s0, (LdsVoid*)dst, 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 2);
+    } else {
+      __builtin_amdgcn_global_load_lds((const void*)s0, (LdsVoid*)dst, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)s1, (LdsVoid*)(dst + 1024), 16, 0, 0);
+    }
   }
   __device__ __forceinline__ uint32_t addr_a(uint32_t slot) const { return ring0 + slot * kPairStride + rd_a; }
   __device__ __forceinline__ uint32_t addr_b(uint32_t slot) const { return ring0 + slot * kPairStride + (rd_a ^ 128u); }
@@ -1691,8 +1802,9 @@ struct PairRing {
 // when `look`) and, after a half-0 slot, refill the pair slot just emptied with pair
 // s / 2 + 2 (of this round, or pair s / 2 + 2 - ns / 2 of the next).
 // Waits: consuming pair P, the DMAs of P + 1 and P + 2 may be in flight (vmcnt(2)); DMAs
-// complete in issue order.
-template <bool kLook>
+// complete in issue order.  kLine: a line round's own pairs 2 .. ns / 2 - 2 (whole lines no
+// neighbour shares) carry the non-temporal hint.
+template <bool kLook, bool kLine = false>
 __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan& cur, const PairPlan& nxt,
                                           PairRing& R, const LaneConsts& c, bool cur_checked, uint32_t& h0,
                                           uint32_t& h1, uint32_t& h2, uint32_t& h3, uint32_t w0, uint32_t w1,
@@ -1710,7 +1822,7 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
     // Pairs 0 and 1 of a round may hold tops (fast rounds: slots B .. B + 1, B <= 1, or any of
     // a 4-slot round's): issued checked, whoever issues them.
     if (f < np)
-      R.issue(cur, f, R.q, cur_checked || f < kPairMinSlots / 2, c);
+      R.issue(cur, f, R.q, cur_checked || f < kPairMinSlots / 2, c, kLine && kLineNT && f >= 2 && f + 1 < np);
     else
       R.issue(nxt, f - np, R.q, true, c);
   } else {
@@ -1719,8 +1831,10 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
 }
 
 // A fast round (tops of every packet in compute slots T .. T + 1, or T .. 3 when NS = 4; no
-// fallback): unrolled; the pairs it issues for itself (P >= 2) need no check.
-template <int NS, int T = 0>
+// fallback): unrolled; the pairs it issues for itself (P >= 2) need no check.  kLine: a line
+// round (line_round_from_record): at the last slot lane 0 masks the words past a1 and the
+// skip mask keeps the streams whose last chunk (or word) lies past E16.
+template <int NS, int T = 0, bool kLine = false>
 __device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
                                                 PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                 uint32_t& h2, uint32_t& h3) {
@@ -1731,12 +1845,21 @@ __device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const Pa
   for (int s = 0; s < NS; ++s) {
     const u32x4 v = R.nextv;
     if (s < T) {
-      pair_step<false>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, 0, 0, 0, 0);
+      pair_step<false, kLine>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, 0, 0, 0, 0);
       issue_order_fence();
       continue;
     }
     uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-    if (s == NS - 1) w3 &= last_word_mask(cur.meta, c.k);  // data only: before the injection in mask_top
+    if (s == NS - 1) {
+      const uint32_t zm = last_word_mask(cur.meta, c.k);  // data only: before the injection in mask_top
+      w3 &= zm;
+      if constexpr (kLine) {  // lane 0: the a1-grid's last word is word 3 - r of the E16 chunk
+        const uint32_t r = (cur.meta >> kMetaLineRShift) & 3u;
+        w2 &= r >= 1u ? zm : 0xFFFFFFFFu;
+        w1 &= r >= 2u ? zm : 0xFFFFFFFFu;
+        w0 &= r >= 3u ? zm : 0xFFFFFFFFu;
+      }
+    }
     if (s <= kMaskEnd) {
       const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
       if (__builtin_amdgcn_ballot_w64(mine)) {
@@ -1748,9 +1871,18 @@ __device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const Pa
       h1 = w1;
       h2 = w2;
       h3 = w3;
-      pair_step<false>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, 0, 0, 0, 0);
+      pair_step<false, kLine>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, 0, 0, 0, 0);
+    } else if (kLine && s == NS - 1) {
+      const uint32_t o0 = h0, o1 = h1, o2 = h2, o3 = h3;
+      pair_step<true, kLine>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, w0, w1, w2, w3);
+      // skip bit i set: stream i keeps o_i (bitop3 0xD8: sel ? o : h)
+      auto keep = [&](int i) { return (uint32_t)((int32_t)(cur.meta << (31 - (int)kMetaSkipShift - i)) >> 31); };
+      h0 = __builtin_amdgcn_bitop3_b32(h0, o0, keep(0), 0xD8);
+      h1 = __builtin_amdgcn_bitop3_b32(h1, o1, keep(1), 0xD8);
+      h2 = __builtin_amdgcn_bitop3_b32(h2, o2, keep(2), 0xD8);
+      h3 = __builtin_amdgcn_bitop3_b32(h3, o3, keep(3), 0xD8);
     } else {
-      pair_step<true>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, w0, w1, w2, w3);
+      pair_step<true, kLine>(s, NS, pc, pn, R, c, false, h0, h1, h2, h3, w0, w1, w2, w3);
     }
     issue_order_fence();
   }
@@ -1765,11 +1897,30 @@ __device__ __forceinline__ bool pair_round_short(const RaggedRound& cur, const P
           ...);
 }
 
+// Line rounds: NS = 8 .. 14 (step counts 8 .. 13), T = 0 or 1.
+__device__ __forceinline__ bool line_round_dispatch(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
+                                                    PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
+                                                    uint32_t& h2, uint32_t& h3) {
+  const int32_t ns = cur.ns();
+  if (cur.top_uniform() == 0) {
+    if (ns == 8) return pair_round_fast<8, 0, true>(cur, pc, pn, R, c, h0, h1, h2, h3), true;
+    if (ns == 10) return pair_round_fast<10, 0, true>(cur, pc, pn, R, c, h0, h1, h2, h3), true;
+    if (ns == 12) return pair_round_fast<12, 0, true>(cur, pc, pn, R, c, h0, h1, h2, h3), true;
+    if (ns == 14) return pair_round_fast<14, 0, true>(cur, pc, pn, R, c, h0, h1, h2, h3), true;
+  } else {
+    if (ns == 10) return pair_round_fast<10, 1, true>(cur, pc, pn, R, c, h0, h1, h2, h3), true;
+    if (ns == 12) return pair_round_fast<12, 1, true>(cur, pc, pn, R, c, h0, h1, h2, h3), true;
+    if (ns == 14) return pair_round_fast<14, 1, true>(cur, pc, pn, R, c, h0, h1, h2, h3), true;
+  }
+  return false;
+}
+
 // Fast rounds of NS = 6, 8, ..., kRaggedFastMax slots, T = 0 or 1.
 template <int... I>
 __device__ __forceinline__ bool pair_round_dispatch(const RaggedRound& cur, const PairPlan& pc, const PairPlan& pn,
                                                     PairRing& R, const LaneConsts& c, uint32_t& h0, uint32_t& h1,
                                                     uint32_t& h2, uint32_t& h3, std::integer_sequence<int, I...>) {
+  if (cur.line()) return line_round_dispatch(cur, pc, pn, R, c, h0, h1, h2, h3);
   if (cur.ns() == kPairMinSlots)
     return pair_round_short(cur, pc, pn, R, c, h0, h1, h2, h3, std::make_integer_sequence<int, kPairMinSlots>{});
   if (cur.top_uniform() == 0)
@@ -2099,6 +2250,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
         const uint32_t h = hdr + 16u * (q >> 3), ns_i = info[i] & kRecStepsMask;
         asm volatile("ds_max_u32 %0, %1\n\tds_min_u32 %0, %1 offset:4" : : "v"(h), "v"(ns_i) : "memory");
         if ((ax[i] >> kRecNearBit) & 1u) lds_or_nowait(h + 8u, 1u);
+        // bit 1: the packet spans nsteps + 1 lines (a line round then needs one slot more)
+        const uint32_t a1l = (uint32_t)ax[i], topl = a1l - (128u * ns_i - ((info[i] >> kRecPadShift) << 2));
+        if (kLineRounds && ((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) == ns_i) lds_or_nowait(h + 8u, 2u);
       }
     }
     // Per round, make_round's rule evaluated once here: hdr.w = ns | B << 26 | fast << 31 (the
@@ -2111,9 +2265,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const bool two_pairs = ns <= kPairMinSlots;  // every pair of the round is issued checked
       const int32_t lim = two_pairs ? ns : B + 1;
       const bool partial = (lane + 1u) * kPacketsPerWave > n;
-      const bool fast = hv.z == 0u && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)hv.y <= (int64_t)lim &&
+      const bool near = (hv.z & 1u) != 0u;
+      const bool fast = !near && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)hv.y <= (int64_t)lim &&
                         (!partial || two_pairs);
-      lds_st32(hdr + 16u * lane + 12u, (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u));
+      // A line round (line_round_from_record): 8 packets of one step count n in kLineMinSteps ..
+      // 13, none near the caller's base.  They span n or n + 1 lines (n + 1 for some: header
+      // bit 1); NS = that maximum rounded up to even, first lines in slots B .. B + 1.
+      // Only when that costs no slot over the end-anchored round (an even n with a packet of
+      // n + 1 lines would need two more: G2 +4 % with them, profiles/r06/line/).
+      const int32_t ml = mx + (int32_t)((hv.z >> 1) & 1u), nl = (ml + 1) & ~1;
+      const bool line = kLineRounds && !near && !partial && hv.y == hv.x && mx >= kLineMinSteps && mx <= 13 && nl == ns;
+      const uint32_t word = line ? (uint32_t)nl | ((uint32_t)(nl - ml) << 26) | 0xC0000000u
+                                 : (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u);
+      lds_st32(hdr + 16u * lane + 12u, word);
     }
     if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
   };
@@ -2169,13 +2333,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     }
     // ns | B << 26 | fast << 31 (job build); a round without records: 4 slots, B = 0, not fast
     const uint32_t hw = rv ? __builtin_amdgcn_readfirstlane(hd.w) : (uint32_t)kPairMinSlots;
-    const bool near_round = __builtin_amdgcn_readfirstlane(hd.z) != 0u;
+    const bool near_round = (__builtin_amdgcn_readfirstlane(hd.z) & 1u) != 0u;  // bit 1: line rounds' extra line
     const int32_t ns = (int32_t)(hw & 0x3FFFFFFu);
     const uint64_t ax0 = axd.x | (uint64_t)axd.y << 32, ax1 = axd.z | (uint64_t)axd.w << 32;
     // Rounds holding a packet near the caller's base (the batch's first few) take their own copy
     // of the decode: the others carry no near-base code at all (one scalar branch).
     RaggedRound rr;
-    if (near_round) {
+    if ((hw >> 30) & 1u) {  // a line round (never near the base, never partial)
+      rr = line_round_from_record(ax, info, (uint32_t)(ax >> kJobLidShift) & 255u, c, hw);
+      rr.plan = line_pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, lane);
+    } else if (near_round) {
       rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u,
                                   c, hw, true);
       rr.plan = pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, dma_off, true, c);
@@ -2282,6 +2449,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     if (!cur.fast() || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
                                           std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{}))
       pair_round_generic(cur, cur.plan, nxt.plan, R, c, lds, h0, h1, h2, h3);
+    if (cur.line()) line_rotate(cur.meta, lane, h0, h1, h2, h3);  // the a1-grid streams of this lane's class
     uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams
     y = apply_rep(lds, y, h2, c.lk.lp1, c.lk);
     y = apply_rep(lds, y, h3, c.lk.lp1, c.lk);

@@ -221,12 +221,13 @@ def test_full_shard_large_32768_x_64k(dev):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("base", [0, 1])
+@pytest.mark.parametrize("base", [0, 1, 3, 100])
 def test_full_size_frag_64k_datagrams(dev, base):
     """the configs[4] bytes as the reference checksums them (bench.py's
     `frag_64k`): 32,768 payloads of 64 KiB, each fragmented at the default MTU into 48
     datagrams of 1392 B and one of 288 B (src/c/peer.rs:181-192), packed back to back from
-    `base`: all 1,605,632 datagrams against the oracle (16 threads)."""
+    `base`: all 1,605,632 datagrams against the oracle (16 threads).  Since round 6 their
+    1392-B rounds are line rounds (bases 0, +1, +3)."""
     n = 32768
     lengths = np.tile(np.array([1392] * 48 + [288], dtype=np.uint32), n)
     offsets = packed_offsets(lengths) + np.uint64(base)
@@ -377,6 +378,49 @@ def test_ragged_mixed_class_rounds(dev, mix):
     offsets = (packed_offsets(lengths) + np.cumsum(rng.integers(0, 4, size=lengths.size))).astype(np.uint64)
     offsets += np.uint64(2)
     data = splitmix64_bytes(63 + len(mix), int(offsets[-1] + lengths[-1]) + 8)
+    got = ragged_on_device(data, offsets, lengths, dev)
+    want = _oracle.crc32_ragged(data, offsets, lengths)
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+
+
+@pytest.mark.parametrize("shape", ["every_step_count", "every_phase_and_gap", "lines_and_ends_mixed",
+                                   "job_boundaries", "overlapping"])
+def test_ragged_line_rounds(dev, shape):
+    """Line rounds (round 6, line_round_from_record; host model tests/test_line_rounds_model.py):
+    rounds of 8 packets of one step count 8..13 run on whole 128-B lines.  every_step_count:
+    each count 8..13 with every start phase 0..127 (so every 16-B end chunk j_last, every
+    grid offset r and every first-word phase); every_phase_and_gap: one length per run of 8,
+    random gaps (packets not back to back); lines_and_ends_mixed: line-eligible runs next to
+    mixed-class and short rounds in the same jobs; job_boundaries: runs of 8 equal step
+    counts that straddle 256-packet jobs, batch ends inside a run (a partial last round is
+    never a line round); overlapping: the same bytes checksummed twice by packets of
+    different rounds."""
+    rng = np.random.default_rng(zlib.crc32(shape.encode()) + 6)
+    if shape == "every_step_count":
+        lengths, gaps = [], []
+        for n in range(8, 14):
+            for ph in range(128):
+                ln = int(rng.integers(128 * (n - 1) + 5, 128 * n - 8))
+                lengths += [ln] * 8
+                gaps += [ph % 7] * 8
+        lengths, gaps = np.array(lengths, dtype=np.uint32), np.array(gaps, dtype=np.uint64)
+    elif shape == "every_phase_and_gap":
+        runs = rng.integers(950, 1700, size=1024)
+        lengths = np.repeat(runs, 8).astype(np.uint32)
+        gaps = rng.integers(0, 64, size=lengths.size).astype(np.uint64)
+    elif shape == "lines_and_ends_mixed":
+        lengths = np.where(rng.random(16384) < 0.6, 1392, rng.integers(0, 1600, size=16384)).astype(np.uint32)
+        gaps = rng.integers(0, 3, size=lengths.size).astype(np.uint64)
+    elif shape == "job_boundaries":
+        lengths = np.repeat(rng.integers(1000, 1700, size=1500), 8)[:4096 * 3 + 5].astype(np.uint32)
+        gaps = np.zeros(lengths.size, dtype=np.uint64)
+    else:
+        lengths = np.full(8192, 1300, dtype=np.uint32)
+        gaps = np.zeros(lengths.size, dtype=np.uint64)
+    offsets = (packed_offsets(lengths) + np.cumsum(gaps)).astype(np.uint64) + np.uint64(int(rng.integers(0, 128)))
+    if shape == "overlapping":
+        offsets = (offsets // np.uint64(2)).astype(np.uint64)  # every byte read by two packets
+    data = splitmix64_bytes(64 + len(shape), int(offsets.max() + lengths.max()) + 8)
     got = ragged_on_device(data, offsets, lengths, dev)
     want = _oracle.crc32_ragged(data, offsets, lengths)
     assert np.array_equal(got, want), int(np.count_nonzero(got != want))

@@ -15,6 +15,7 @@
 //   8x128 regs   the 8-lane shape loaded into a register ring (3 or 6 deep; nt: non-temporal)
 //   8x256x2 d2/3 8 packets x 256 B per 2-KiB slot as two 4 x 256-B instructions (the round-5 plan)
 //   4x256x1 d4, 8x256x2 d1, 4x512x2 d2, 2x512x1 d4: the same bytes in flight with other packet counts
+//   ... nt: the LDS-DMA shapes with the non-temporal hint (round 6)
 // Workgroups of 1024 threads, one per CU (the LDS is padded to the kernels' 150 KiB), a
 // persistent grid over static rounds.  Alternating blocks of 20 launches per shape after a
 // warm-up; prints us per launch and GB/s.  Addresses stay inside the buffer: the packets
@@ -52,7 +53,7 @@ __device__ __forceinline__ u32x4 read_lds(uint32_t addr) {
 }
 
 // P packets per round, PIECE bytes per packet per slot, I instructions per slot, ring of D.
-template <int P, int PIECE, int I, int D>
+template <int P, int PIECE, int I, int D, int kAux = 0>
 __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32_t L, uint64_t rounds,
                                                      uint64_t amask, uint32_t* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32
   for (int d = 0; d < D; ++d) {
 #pragma unroll
     for (int i = 0; i < I; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)src(dj, dsl, i), (LdsVoid*)(lds + ring_addr(d, i)), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src(dj, dsl, i), (LdsVoid*)(lds + ring_addr(d, i)), 16, 0, kAux);
     advance();
   }
   uint32_t pos = 0;
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(1024) void shape_kernel(const uint8_t* base, uint32
     for (int i = 1; i < I; ++i) acc ^= read_lds(ring_addr(pos, i) + 16 * lane);
 #pragma unroll
     for (int i = 0; i < I; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)src(dj, dsl, i), (LdsVoid*)(lds + ring_addr(pos, i)), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src(dj, dsl, i), (LdsVoid*)(lds + ring_addr(pos, i)), 16, 0, kAux);
     advance();
     pos = pos + 1 == D ? 0 : pos + 1;
   }
@@ -172,9 +173,9 @@ void launch_regs(int grid, const uint8_t* b, uint32_t L, uint64_t rounds, uint64
   hipLaunchKernelGGL((shape_regs_kernel<P, PIECE, D, kNT>), dim3(grid), dim3(1024), 0, 0, b, L, rounds, amask, out);
 }
 
-template <int P, int PIECE, int I, int D>
+template <int P, int PIECE, int I, int D, int kAux = 0>
 void launch_shape(int grid, const uint8_t* b, uint32_t L, uint64_t rounds, uint64_t amask, uint32_t* out) {
-  hipLaunchKernelGGL((shape_kernel<P, PIECE, I, D>), dim3(grid), dim3(1024), 0, 0, b, L, rounds, amask, out);
+  hipLaunchKernelGGL((shape_kernel<P, PIECE, I, D, kAux>), dim3(grid), dim3(1024), 0, 0, b, L, rounds, amask, out);
 }
 
 #define CHECK(x)                                                             \
@@ -209,6 +210,10 @@ int main(int argc, char** argv) {
       // round-5 additions: in-flight bytes vs packets per wave
       {"4x256x1 d4", 4, launch_shape<4, 256, 1, 4>},   {"8x256x2 d1", 8, launch_shape<8, 256, 2, 1>},
       {"4x512x2 d2", 4, launch_shape<4, 512, 2, 2>},   {"2x512x1 d4", 2, launch_shape<2, 512, 1, 4>},
+      // round-6 additions: the LDS-DMA shapes with the non-temporal hint (aux 2, as the uniform DMA kernels)
+      {"8x256x2 d2 nt", 8, launch_shape<8, 256, 2, 2, 2>}, {"8x128x1 d3 nt", 8, launch_shape<8, 128, 1, 3, 2>},
+      {"4x256x1 d2 nt", 4, launch_shape<4, 256, 1, 2, 2>}, {"8x256x2 d1 nt", 8, launch_shape<8, 256, 2, 1, 2>},
+      {"8x128x1 d6 nt", 8, launch_shape<8, 128, 1, 6, 2>}, {"8x128x1 d4 nt", 8, launch_shape<8, 128, 1, 4, 2>},
   };
   const int ns = sizeof(shapes) / sizeof(shapes[0]);
   hipDeviceProp_t prop;
