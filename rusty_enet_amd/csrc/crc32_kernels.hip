@@ -1516,16 +1516,18 @@ struct RaggedRound {
   uint32_t id;          // packet id (output index)
   // Wave-uniform, one SGPR each (the loop carries two rounds; every SGPR it carries is one the
   // job build and the round bodies cannot use, and the kernel is at the 106-SGPR limit):
-  uint32_t hw;          // the round header's word (job build): ns | B << 26 | line << 30 | fast << 31
+  uint32_t hw;          // the round header's word (job build): ns | B << 26 | rot << 29 | line << 30 | fast << 31
   uint32_t d;           // the workgroup's round index (live, job number and job rounds follow from it)
   PairPlan plan;        // this lane's DMA plan for the round
   __device__ int32_t ns() const { return (int32_t)(hw & 0x3FFFFFFu); }  // slots of the round
   // B: the first top slot of a fast round (any of 0 .. 3 when ns == kPairMinSlots)
-  __device__ int32_t top_uniform() const { return (int32_t)((hw >> 26) & 15u); }
+  __device__ int32_t top_uniform() const { return (int32_t)((hw >> 26) & 7u); }
   // top slots in B .. B + 1 (any in 4-slot rounds), no fallback, ns <= kRaggedFastMax
   __device__ bool fast() const { return (int32_t)hw < 0; }
   // a line round (line_round_from_record): whole-line slots, always fast
   __device__ bool line() const { return ((hw >> 30) & 1u) != 0u; }
+  // a line round where some packet's a1 is not on the 16-B grid (r != 0: line_rotate, word masks)
+  __device__ bool line_rot() const { return ((hw >> 29) & 1u) != 0u; }
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kPairMinSlots .. kRaggedFastMax
@@ -1853,7 +1855,7 @@ __device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const Pa
     if (s == NS - 1) {
       const uint32_t zm = last_word_mask(cur.meta, c.k);  // data only: before the injection in mask_top
       w3 &= zm;
-      if constexpr (kLine) {  // lane 0: the a1-grid's last word is word 3 - r of the E16 chunk
+      if (kLine && cur.line_rot()) {  // lane 0: the a1-grid's last word is word 3 - r of the E16 chunk
         const uint32_t r = (cur.meta >> kMetaLineRShift) & 3u;
         w2 &= r >= 1u ? zm : 0xFFFFFFFFu;
         w1 &= r >= 2u ? zm : 0xFFFFFFFFu;
@@ -2253,6 +2255,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
         // bit 1: the packet spans nsteps + 1 lines (a line round then needs one slot more)
         const uint32_t a1l = (uint32_t)ax[i], topl = a1l - (128u * ns_i - ((info[i] >> kRecPadShift) << 2));
         if (kLineRounds && ((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) == ns_i) lds_or_nowait(h + 8u, 2u);
+        // bit 2: its a1 is not on the 16-B grid (a line round then exchanges words, line_rotate)
+        if (kLineRounds && (a1l & 12u)) lds_or_nowait(h + 8u, 4u);
       }
     }
     // Per round, make_round's rule evaluated once here: hdr.w = ns | B << 26 | fast << 31 (the
@@ -2275,7 +2279,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       // n + 1 lines would need two more: G2 +4 % with them, profiles/r06/line/).
       const int32_t ml = mx + (int32_t)((hv.z >> 1) & 1u), nl = (ml + 1) & ~1;
       const bool line = kLineRounds && !near && !partial && hv.y == hv.x && mx >= kLineMinSteps && mx <= 13 && nl == ns;
-      const uint32_t word = line ? (uint32_t)nl | ((uint32_t)(nl - ml) << 26) | 0xC0000000u
+      const uint32_t word = line ? (uint32_t)nl | ((uint32_t)(nl - ml) << 26) | ((hv.z & 4u) << 27) | 0xC0000000u
                                  : (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u);
       lds_st32(hdr + 16u * lane + 12u, word);
     }
@@ -2449,7 +2453,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     if (!cur.fast() || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
                                           std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{}))
       pair_round_generic(cur, cur.plan, nxt.plan, R, c, lds, h0, h1, h2, h3);
-    if (cur.line()) line_rotate(cur.meta, lane, h0, h1, h2, h3);  // the a1-grid streams of this lane's class
+    if (cur.line() && cur.line_rot()) line_rotate(cur.meta, lane, h0, h1, h2, h3);  // this lane's a1-grid streams
     uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams
     y = apply_rep(lds, y, h2, c.lk.lp1, c.lk);
     y = apply_rep(lds, y, h3, c.lk.lp1, c.lk);
