@@ -40,6 +40,7 @@
 //                 32 different banks.  Each address is ONE v_perm_b32.
 //   [64 KiB, +)   unreplicated tree operators M32^4/8/16.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1755,11 +1756,15 @@ __device__ __forceinline__ void line_rotate(uint32_t meta, uint32_t lane, uint32
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(n1), "=&v"(n2), "=&v"(n3)
       : "v"(src), "v"(h1), "v"(h2), "v"(h3));
-  const uint32_t r = (meta >> kMetaLineRShift) & 3u;
-  const uint32_t g0 = r == 0u ? h0 : (r == 1u ? n3 : (r == 2u ? n2 : n1));
-  const uint32_t g1 = r == 0u ? h1 : (r == 1u ? h0 : (r == 2u ? n3 : n2));
-  const uint32_t g2 = r == 0u ? h2 : (r == 1u ? h1 : (r == 2u ? h0 : n3));
-  const uint32_t g3 = r == 0u ? h3 : (r == 1u ? h2 : (r == 2u ? h1 : h0));
+  // 4-way select by r as two bitop3 muxes per bit of r (0xD8: c ? b : a); as ternaries hipcc
+  // made EXEC-masked branches of them.
+  const uint32_t m0 = (uint32_t)((int32_t)(meta << (31 - kMetaLineRShift)) >> 31);      // r & 1
+  const uint32_t m1 = (uint32_t)((int32_t)(meta << (31 - kMetaLineRShift - 1)) >> 31);  // r & 2
+  auto pick = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32(x0, x1, m0, 0xD8), hi = __builtin_amdgcn_bitop3_b32(x2, x3, m0, 0xD8);
+    return __builtin_amdgcn_bitop3_b32(lo, hi, m1, 0xD8);
+  };
+  const uint32_t g0 = pick(h0, n3, n2, n1), g1 = pick(h1, h0, n3, n2), g2 = pick(h2, h1, h0, n3), g3 = pick(h3, h2, h1, h0);
   h0 = g0;
   h1 = g1;
   h2 = g2;
@@ -1864,9 +1869,7 @@ __device__ __forceinline__ void pair_round_fast(const RaggedRound& cur, const Pa
     }
     if (s <= kMaskEnd) {
       const bool mine = cur.top_slot == s && (cur.meta & kMetaHeadMask);
-      if (__builtin_amdgcn_ballot_w64(mine)) {
-        if (mine) mask_top_lds(cur.meta, R.topmask, w0, w1, w2, w3);
-      }
+      if (mine) mask_top_lds(cur.meta, R.topmask, w0, w1, w2, w3);  // EXEC-masked; skipped when no lane
     }
     if (s == T) {
       h0 = w0;  // first top slot: every stream is still zero (M32^32(0) = 0), no lookups
@@ -2029,6 +2032,12 @@ struct RaggedJobsLds {
   uint32_t res_dummy[64];        // publish(): where the lanes that hold no checksum store theirs
 };
 static_assert(sizeof(RaggedJobsLds) <= 160 * 1024, "LDS");
+// LDS byte addresses of the jobs kernel's variables as constants: its one __shared__ object
+// starts at LDS address 0 (checked at the kernel's start), so a member's address is its
+// offset.  (Casting a member's generic address to the LDS space costs a null test per use,
+// s_cmp_lg_u64 + s_cselect, and keeps the object's 64-bit generic address in two SGPRs.)
+#define ENET_S_OFF(m) ((uint32_t)offsetof(RaggedJobsLds, m))
+__device__ __forceinline__ uint32_t job_off(uint32_t slot) { return ENET_S_OFF(job) + slot * (uint32_t)sizeof(JobSlot); }
 
 struct RaggedJobsBatch {
   uint64_t base;
@@ -2070,7 +2079,7 @@ __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
   asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(old) : "v"(a), "v"(v) : "memory");
   return old;
 }
-__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(LdsVoid*)p; }
+
 // No-return add, not waited for (the next asm wait on lgkmcnt covers it).
 __device__ __forceinline__ void lds_add_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_add_u32 %0, %1" : : "v"(a), "v"(v) : "memory");
@@ -2195,14 +2204,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   // write its round records in place of the descriptors; then mark the slot ready.
   auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
     asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDescWait) : "memory");
-    const uint32_t st = lds_addr(&S.job[slot].rec[0]);
+    const uint32_t st = (job_off(slot) + (uint32_t)offsetof(JobSlot, rec));
     const u32x4 o01 = lds_ld128(st + 32u * lane), o23 = lds_ld128(st + 32u * lane + 16u);
     const u32x4 ln = lds_ld128(st + 2048u + 16u * lane);
     const uint64_t off[4] = {o01.x | (uint64_t)o01.y << 32, o01.z | (uint64_t)o01.w << 32,
                              o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
     const uint32_t len[4] = {ln.x, ln.y, ln.z, ln.w};
     const uint32_t n = job_count(J);
-    const uint32_t hdr = lds_addr(&S.job[slot].hdr[0]);
+    const uint32_t hdr = (job_off(slot) + (uint32_t)offsetof(JobSlot, hdr));
     if (lane < (uint32_t)kJobRounds) {  // max 0, min ~0, flags 0; in order before the atomics below
       asm volatile("ds_write_b128 %0, %1" : : "v"(hdr + 16u * lane), "v"(u32x4{0u, 0xFFFFFFFFu, 0u, 0u}) : "memory");
     }
@@ -2283,7 +2292,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
                                  : (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u);
       lds_st32(hdr + 16u * lane + 12u, word);
     }
-    if (lane == 0) lds_st32(lds_addr(&S.ready[slot]), gen);
+    if (lane == 0) lds_st32((ENET_S_OFF(ready) + 4u * slot), gen);
   };
 
   // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
@@ -2299,7 +2308,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 
   // Jobs this wave has seen ready / flushed (a job's flags are polled once per wave).
   uint32_t seen_ready = 0, seen_freed = 0;
-  const uint32_t fail_a = lds_addr(&S.failed);
+  const uint32_t fail_a = ENET_S_OFF(failed);
   // This lane's offset inside the 256-B pieces of its DMA packets (PairRing).
   const uint32_t dma_off = 128u * (((lane >> 3) ^ (lane >> 4)) & 1u) + 16u * (lane & 7u);
   // A wait's outcome: true if the flag came; a wave's own time-out is reported.
@@ -2313,7 +2322,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint32_t k = div_rj(d), slot = k % kJobSlots;
     bool rv = d < wg_rounds;  // round_valid(d)
     if (rv && k + 1u > seen_ready) {
-      rv = waited(lds_wait_eq(lds_addr(&S.ready[slot]), k + 1u, fail_a), kFaultReady);
+      rv = waited(lds_wait_eq((ENET_S_OFF(ready) + 4u * slot), k + 1u, fail_a), kFaultReady);
       if (rv) seen_ready = k + 1u;
     }
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2323,7 +2332,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     uint64_t infod = 0;
     u32x4 hd = {0, 0, 0, 0};   // the round header: max steps, min steps, near flag
     if (rv) {
-      const uint32_t r = lds_addr(&S.job[slot].rec[0]) + (d - k * RJ) * kJobRoundBytes;
+      const uint32_t r = (job_off(slot) + (uint32_t)offsetof(JobSlot, rec)) + (d - k * RJ) * kJobRoundBytes;
       const uint32_t gd = lane >> 4;
       asm volatile(  // one round trip
           "ds_read_b64 %0, %5\n\tds_read_b32 %1, %6\n\t"
@@ -2331,9 +2340,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
           "ds_read_b128 %4, %9\n\ts_waitcnt lgkmcnt(0)"
           : "=&v"(ax), "=&v"(info), "=&v"(axd), "=&v"(infod), "=&v"(hd)
           : "v"(r + 8u * c.grp), "v"(r + 64u + 4u * c.grp), "v"(r + 8u * gd), "v"(r + 64u + 4u * gd),
-            "v"(lds_addr(&S.job[slot].hdr[0]) + 16u * (d - k * RJ))
+            "v"((job_off(slot) + (uint32_t)offsetof(JobSlot, hdr)) + 16u * (d - k * RJ))
           : "memory");
-      if (lane == 0) lds_add_nowait(lds_addr(&S.consumed[slot]), 1u);
+      if (lane == 0) lds_add_nowait((ENET_S_OFF(consumed) + 4u * slot), 1u);
     }
     // ns | B << 26 | fast << 31 (job build); a round without records: 4 slots, B = 0, not fast
     const uint32_t hw = rv ? __builtin_amdgcn_readfirstlane(hd.w) : (uint32_t)kPairMinSlots;
@@ -2366,7 +2375,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // writes the job's checksums to HBM.
     const uint32_t slot0 = k0 % kJobSlots;
     if (k0 >= (uint32_t)kJobSlots && k0 + 1u - (uint32_t)kJobSlots > seen_freed) {
-      if (waited(lds_wait_eq(lds_addr(&S.freed[slot0]), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
+      if (waited(lds_wait_eq((ENET_S_OFF(freed) + 4u * slot0), k0 - (uint32_t)kJobSlots + 1u, fail_a), kFaultFreed))
         seen_freed = k0 + 1u - (uint32_t)kJobSlots;
     }
 #ifdef ENET_CRC_TEST_HOOKS
@@ -2378,18 +2387,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     {  // every lane stores: lane k == 0 of a valid packet into res[id], the others into res_dummy
       const uint32_t sel = (uint32_t)((int32_t)(meta << (31 - 10)) >> 31) &  // kMetaStore (bit 10)
                            (uint32_t)((int32_t)(c.k - 1u) >> 31);            // k == 0
-      const uint32_t ra = lds_addr(&S.job[slot0].res[0]) + 4u * id, da = lds_addr(&S.res_dummy[0]) + 4u * lane;
+      const uint32_t ra = (job_off(slot0) + (uint32_t)offsetof(JobSlot, res)) + 4u * id, da = ENET_S_OFF(res_dummy) + 4u * lane;
       lds_st32_nowait((sel & ra) | (~sel & da), __builtin_bswap32(~reg));
     }
     uint32_t old = 0;
-    if (lane == 0) old = lds_add_rtn(lds_addr(&S.done[slot0]), 1u);
+    if (lane == 0) old = lds_add_rtn((ENET_S_OFF(done) + 4u * slot0), 1u);
     old = __builtin_amdgcn_readfirstlane(old);
     // After a failure in the workgroup nothing more is flushed: a job whose records or
     // result slot were skipped would leave stale checksums in res[].
     if (old + 1u == job_rounds && __builtin_amdgcn_readfirstlane(lds_ld32(fail_a)) == 0u) {
       const uint64_t J0 = job_of(k0);
       const uint32_t n0 = job_count(J0);
-      const u32x4 v = lds_ld128(lds_addr(&S.job[slot0].res[0]) + 16u * lane);
+      const u32x4 v = lds_ld128((job_off(slot0) + (uint32_t)offsetof(JobSlot, res)) + 16u * lane);
       uint32_t* dst = out + J0 * JP + 4u * lane;
       if (4u * lane + 4u <= n0) {
         reinterpret_cast<U32x4A4*>(dst)->v = v;
@@ -2401,8 +2410,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     }
     if (old + 1u == job_rounds) {
       if (lane == 0) {
-        lds_st32(lds_addr(&S.done[slot0]), 0u);
-        lds_st32(lds_addr(&S.freed[slot0]), k0 + 1u);
+        lds_st32((ENET_S_OFF(done) + 4u * slot0), 0u);
+        lds_st32((ENET_S_OFF(freed) + 4u * slot0), k0 + 1u);
       }
     }
   };
@@ -2411,8 +2420,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   RaggedRound nxt = make_round(wv + kWavesPerBlock);
   PairRing R;
   R.slot0 = (LdsVoid*)&S.ring[0][wv][0];
-  R.ring0 = lds_addr(&S.ring[0][wv][0]);
-  R.topmask = lds_addr(&S.topmask[0]);
+  R.ring0 = (ENET_S_OFF(ring) + wv * kPairBytes);
+  R.topmask = ENET_S_OFF(topmask);
   {
     const uint32_t g = lane >> 3, k = lane & 7u, j = g & 3u;
     R.rd_a = 1024u * (g >> 2) + 256u * j + 128u * (j & 1u) + 16u * (7u - k);
@@ -2424,7 +2433,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   uint32_t tree_a = 0x10000u;  // tree_levels_asm's address register (high half 1, kept)
   while (cur.d < wg_rounds) {  // the current round is inside the batch
     uint32_t d = 0;
-    if (lane == 0) d = lds_add_rtn(lds_addr(&S.next_dispatch), 1u);
+    if (lane == 0) d = lds_add_rtn(ENET_S_OFF(next_dispatch), 1u);
     d = __builtin_amdgcn_readfirstlane(d);
     // Build duty: the claimer of a job's first round builds the job kJobAhead later (the
     // prologue built the first ones) once every round of the slot's previous job has read
@@ -2435,13 +2444,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     const uint32_t kd = div_rj(d), kb = kd + kJobAhead, bslot = kb % kJobSlots;
     if (d == kd * RJ && kb >= first_jobs && kb < wg_jobs) {  // rare: the first round of a job
       build = kb < (uint32_t)kJobSlots ||
-              waited(lds_wait_eq(lds_addr(&S.consumed[bslot]), RJ, fail_a), kFaultConsumed);
+              waited(lds_wait_eq((ENET_S_OFF(consumed) + 4u * bslot), RJ, fail_a), kFaultConsumed);
 #ifdef ENET_CRC_TEST_HOOKS
       if (blockIdx.x == 0 && kb >= (uint32_t)kJobSlots && kb + 1u == b.fault_k && b.fault_kind == kFaultConsumed)
         build = waited(kWaitGaveUp, kFaultConsumed);
 #endif
       if (build) {
-        if (lane == 0) lds_st32(lds_addr(&S.consumed[bslot]), 0u);
+        if (lane == 0) lds_st32((ENET_S_OFF(consumed) + 4u * bslot), 0u);
         job_dma(job_of(kb), bslot);
       }
     }
