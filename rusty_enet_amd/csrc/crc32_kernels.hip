@@ -1532,18 +1532,7 @@ struct RaggedRound {
 };
 
 constexpr int kRaggedFastMax = 14;  // unrolled round bodies for ns = kPairMinSlots .. kRaggedFastMax
-#ifndef ENET_CRC_LINE_ROUNDS
-#define ENET_CRC_LINE_ROUNDS 1
-#endif
-constexpr bool kLineRounds = ENET_CRC_LINE_ROUNDS != 0;  // line_round_from_record (0: A/B builds)
-#ifndef ENET_CRC_LINE_MIN_STEPS
-#define ENET_CRC_LINE_MIN_STEPS 8
-#endif
-#ifndef ENET_CRC_LINE_NT
-#define ENET_CRC_LINE_NT 1
-#endif
-constexpr int kLineMinSteps = ENET_CRC_LINE_MIN_STEPS;    // the shortest packets a line round holds
-constexpr bool kLineNT = ENET_CRC_LINE_NT != 0;           // interior pairs of line rounds non-temporal
+constexpr int kLineMinSteps = 8;  // the shortest packets a line round holds (10: level, profiles/r06/line/)
 
 // ---------------------------------------------------------------------------------
 // Ragged rounds with 256-B loads.  The arithmetic and the compute
@@ -1561,11 +1550,7 @@ constexpr bool kLineNT = ENET_CRC_LINE_NT != 0;           // interior pairs of l
 // flight.  The DMA lane decides per 16-B chunk whether it is real (at or after its packet's
 // top word, not below the caller's buffer) or the zero chunk.
 // ---------------------------------------------------------------------------------
-#ifndef ENET_CRC_PAIR_RING
-#define ENET_CRC_PAIR_RING 2
-#endif
-constexpr int kPairRing = ENET_CRC_PAIR_RING;                   // pair slots per wave (1 or 2)
-static_assert(kPairRing == 1 || kPairRing == 2, "pair ring");
+constexpr int kPairRing = 2;                                    // pair slots per wave
 // Lane k == 0 clears the z bytes past its packet's end in the last word (z in meta).
 __device__ __forceinline__ uint32_t last_word_mask(uint32_t meta, uint32_t k) {
   // No lane compare (hipcc hoists k == 0 into a lane mask, then spills it to a VGPR lane):
@@ -1817,8 +1802,8 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
                                           uint32_t& h1, uint32_t& h2, uint32_t& h3, uint32_t w0, uint32_t w1,
                                           uint32_t w2, uint32_t w3) {
   const bool half0 = (s & 1) == 0;
-  const uint32_t next_addr = half0 ? R.addr_b(R.q) : R.addr_a(kPairRing == 2 ? R.q ^ 1u : R.q);
-  constexpr int kWait = 2 * (kPairRing - 1);  // the two DMAs of the pair after the one read may stay in flight
+  const uint32_t next_addr = half0 ? R.addr_b(R.q) : R.addr_a(R.q ^ 1u);
+  constexpr int kWait = 2;  // the two DMAs of the pair after the one read may stay in flight
   if constexpr (kLook) {
     horner_step_and_read<kWait>(c.lk, h0, h1, h2, h3, w0, w1, w2, w3, next_addr, R.nextv);
   } else {
@@ -1829,11 +1814,11 @@ __device__ __forceinline__ void pair_step(int32_t s, int32_t ns, const PairPlan&
     // Pairs 0 and 1 of a round may hold tops (fast rounds: slots B .. B + 1, B <= 1, or any of
     // a 4-slot round's): issued checked, whoever issues them.
     if (f < np)
-      R.issue(cur, f, R.q, cur_checked || f < kPairMinSlots / 2, c, kLine && kLineNT && f >= 2 && f + 1 < np);
+      R.issue(cur, f, R.q, cur_checked || f < kPairMinSlots / 2, c, kLine && f >= 2 && f + 1 < np);
     else
       R.issue(nxt, f - np, R.q, true, c);
   } else {
-    if (kPairRing == 2) R.q ^= 1u;
+    R.q ^= 1u;
   }
 }
 
@@ -2263,9 +2248,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
         if ((ax[i] >> kRecNearBit) & 1u) lds_or_nowait(h + 8u, 1u);
         // bit 1: the packet spans nsteps + 1 lines (a line round then needs one slot more)
         const uint32_t a1l = (uint32_t)ax[i], topl = a1l - (128u * ns_i - ((info[i] >> kRecPadShift) << 2));
-        if (kLineRounds && ((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) == ns_i) lds_or_nowait(h + 8u, 2u);
+        if (((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) == ns_i) lds_or_nowait(h + 8u, 2u);
         // bit 2: its a1 is not on the 16-B grid (a line round then exchanges words, line_rotate)
-        if (kLineRounds && (a1l & 12u)) lds_or_nowait(h + 8u, 4u);
+        if ((a1l & 12u)) lds_or_nowait(h + 8u, 4u);
       }
     }
     // Per round, make_round's rule evaluated once here: hdr.w = ns | B << 26 | fast << 31 (the
@@ -2287,7 +2272,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       // Only when that costs no slot over the end-anchored round (an even n with a packet of
       // n + 1 lines would need two more: G2 +4 % with them, profiles/r06/line/).
       const int32_t ml = mx + (int32_t)((hv.z >> 1) & 1u), nl = (ml + 1) & ~1;
-      const bool line = kLineRounds && !near && !partial && hv.y == hv.x && mx >= kLineMinSteps && mx <= 13 && nl == ns;
+      const bool line = !near && !partial && hv.y == hv.x && mx >= kLineMinSteps && mx <= 13 && nl == ns;
       const uint32_t word = line ? (uint32_t)nl | ((uint32_t)(nl - ml) << 26) | ((hv.z & 4u) << 27) | 0xC0000000u
                                  : (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u);
       lds_st32(hdr + 16u * lane + 12u, word);
@@ -2428,8 +2413,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     R.dma_off = dma_off;
   }
   R.q = 0;
-  for (int P = 0; P < kPairRing; ++P) R.issue(cur.plan, P, (uint32_t)P, true, c);  // cur.ns >= kPairMinSlots
-  R.nextv = read_landed_slot<2 * (kPairRing - 1)>(R.addr_a(0));
+  R.issue(cur.plan, 0, 0, true, c);  // cur.ns >= kPairMinSlots: pairs 0 and 1
+  R.issue(cur.plan, 1, 1, true, c);
+  R.nextv = read_landed_slot<2>(R.addr_a(0));
   uint32_t tree_a = 0x10000u;  // tree_levels_asm's address register (high half 1, kept)
   while (cur.d < wg_rounds) {  // the current round is inside the batch
     uint32_t d = 0;
