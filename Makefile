@@ -68,9 +68,14 @@ tests/cpp/bin/host_asan: tests/cpp/host_asan.cpp oracle/crc32_oracle.c oracle/ra
 
 .PHONY: asan
 
-# Measurement probes (tooling, not product): tools/dma_probe.
-probes: tools/dma_probe
+# Measurement probes (tooling, not product): tools/dma_probe, and round 6's
+# load-shape probes tools/dma_shape, tools/shape_arith, tools/lines_probe.
+probes: tools/dma_probe tools/dma_shape tools/shape_arith tools/lines_probe
 tools/dma_probe: tools/dma_probe.hip rusty_enet_amd/csrc/crc32_layout.hpp rusty_enet_amd/csrc/crc32_ops.hpp
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++20 -o $@ tools/dma_probe.hip
+tools/dma_shape: tools/dma_shape.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ tools/dma_shape.hip
+tools/shape_arith tools/lines_probe: tools/%: tools/%.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++20 -o $@ $<
 
 .PHONY: probes
