@@ -267,7 +267,8 @@ constexpr uint32_t kMetaTShiftShift = 8;      // 2 bits: first trailing byte's p
 constexpr uint32_t kMetaStore = 1u << 10;     // packet index < count
 constexpr uint32_t kMetaFallback = 1u << 11;  // top chunk begins before the caller's buffer
 constexpr uint32_t kMetaDirect = 1u << 12;    // ragged rounds: the top chunk is read directly (inside, no fallback)
-constexpr uint32_t kMetaLineRShift = 13;      // line rounds: 2 bits, r = (E16 - a1) / 4 words
+constexpr uint32_t kMetaLineRShift = 8;       // line rounds: 2 bits, r = (E16 - a1) / 4 words (ragged rounds
+                                              // never use kMetaTShiftShift's field)
 constexpr uint32_t kMetaSkipShift = 15;       // line rounds: 4 bits, words not multiplied in at the last slot
 constexpr uint32_t kHeadZero = 5;             // line rounds: head code of a chunk wholly before the first word
 
@@ -665,6 +666,7 @@ constexpr uint64_t kRecAddrMask = (1ull << 48) - 1;
 constexpr int kRecVShift = 48, kRecZShift = 50, kRecNearBit = 52, kRecValidBit = 53;
 constexpr uint32_t kRecStepsMask = (1u << 26) - 1;
 constexpr int kRecPadShift = 26;
+constexpr int kJobLidShift = 54;  // job build: the packet's local id (0..255) in ax bits 54..61
 struct RaggedRecord {
   uint64_t ax;
   uint32_t info;
@@ -1647,7 +1649,8 @@ __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint3
   RaggedRound rr;
   rr.hw = hw;
   const int32_t ns = rr.ns();
-  rr.cb = a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(ns - 1);
+  // The top chunk's address, for the fallback load (near-base rounds only; unused otherwise).
+  rr.cb = near_round ? a1 - 16u * (uint64_t)(c.k + 1u) - (uint64_t)kBytesPerStep * (uint64_t)(ns - 1) : 0ull;
   rr.top_slot = ns - nsteps;
   const int32_t rel = 112 - 16 * (int32_t)c.k - (int32_t)pad;
   const bool inside = nsteps > 0 && rel > -16;
@@ -1686,46 +1689,118 @@ __device__ __forceinline__ RaggedRound pair_round_from_record(uint64_t ax, uint3
 //     (line_rotate; lane 7 takes lane 0's skipped words, one stream step behind);
 //   * at its first line each lane masks its chunk from the mask table: before the first
 //     word (kHeadZero), the first word's chunk (head, v: the init register injected), or none.
-// Line and chunk indices use the addresses' low 32 bits (a packet spans < 2^25 lines).
-__device__ __forceinline__ RaggedRound line_round_from_record(uint64_t ax, uint32_t info, uint32_t id,
-                                                              const LaneConsts& c, uint32_t hw) {
-  const uint32_t a1l = (uint32_t)ax;
-  const uint32_t nsteps = info & kRecStepsMask, pad = (info >> kRecPadShift) << 2;
+// ---------------------------------------------------------------------------------
+// Packed round records (round 6; host model: tests/test_packed_records_model.py).  Once a
+// job's round headers are complete, job_build writes the records of fast and line rounds in
+// a form that already holds the round's slot count: what every lane of the round derives
+// from it (its top slot and head code; each DMA lane's pair-0 address and first real pair)
+// then costs a few instructions in make_round, instead of the full decode of the raw record
+// per lane and round (8 lanes decode each packet, and each record is read by 3 lanes x its
+// round; the build packs it once).  Generic and near-base rounds keep the raw record.
+//   Fast rounds (format A, NS <= 14):
+//     X = piece0 (48 bits: a1 - 128 NS) | W << 48,  W = 128 (NS - nsteps) + pad + 240 (12 bits)
+//         -> db = piece0 + dma_off, first pair = (W - dma_off) >> 8 (pair_plan's formula)
+//     Y = the meta of lane k_t (head h_t, v, empty, z, store) | k_t << 13 | top slot << 16 | id << 24
+//         k_t = (127 - pad) >> 4 is the lane whose chunk holds the top word; the others' head is 0.
+//   Line rounds (format B):
+//     X = L (48 bits: the last line - 128 (NS - 1)) | j_last << 48 | x << 51 | m << 55,
+//         x = NS - lines (the top slot), m = meta bits 3..9 (v, 0, z, r)
+//     Y = head table (3 bits per lane k: kHeadZero, 4 - wt or 0) | id << 24
+// Line and chunk indices use the addresses' low 32 bits (a packet spans < 2^25 lines).  GPU
+// virtual addresses of packets are far above 1792 B, so piece0 and L never wrap below 0.
+// ---------------------------------------------------------------------------------
+constexpr int kPkWShift = 48;
+constexpr uint32_t kPkKtShift = 13, kPkTopShift = 16, kPkIdShift = 24;
+constexpr uint32_t kPkJlShift = 16, kPkXShift = 19, kPkMetaShift = 23;  // format B, in X's high word
+
+// Format A from a raw record (valid: a packet is at this position; else ax = info = 0).
+__device__ __forceinline__ void pack_fast(uint64_t ax, uint32_t info, bool valid, uint32_t ns, uint64_t& X,
+                                          uint32_t& Y) {
+  const uint64_t a1 = ax & kRecAddrMask;
+  const uint32_t nsteps = valid ? info & kRecStepsMask : 0u, pad = valid ? (info >> kRecPadShift) << 2 : 0u;
+  const uint32_t v = (uint32_t)(ax >> kRecVShift) & 3u, z = (uint32_t)(ax >> kRecZShift) & 3u;
+  const uint32_t id = (uint32_t)(ax >> kJobLidShift) & 255u;
+  const uint32_t W = 128u * (ns - nsteps) + pad + 240u;
+  X = ((a1 - (uint64_t)kBytesPerStep * ns) & kRecAddrMask) | ((uint64_t)W << kPkWShift);
+  const uint32_t kt = (127u - pad) >> 4;                    // rel = 112 - 16 k - pad in (-16, 0]
+  const uint32_t ht = nsteps ? 32u - 4u * kt - (pad >> 2) : 0u;  // rel / 4 + 4
+  Y = ht | (v << kMetaVShift) | (nsteps == 0 ? kMetaEmpty : 0u) | (z << kMetaNTailShift) |
+      (valid ? kMetaStore : 0u) | (kt << kPkKtShift) | ((ns - nsteps) << kPkTopShift) | (id << kPkIdShift);
+}
+
+// Format B from a raw record of a line round (every position valid, NS = the round's slots).
+__device__ __forceinline__ void pack_line(uint64_t ax, uint32_t info, uint32_t ns, uint64_t& X, uint32_t& Y) {
+  const uint64_t a1 = ax & kRecAddrMask;
+  const uint32_t a1l = (uint32_t)a1, nsteps = info & kRecStepsMask, pad = (info >> kRecPadShift) << 2;
   const uint32_t topl = a1l - (128u * nsteps - pad);
   const uint32_t lines = ((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) + 1u;
+  const uint32_t j_last = ((a1l - 1u) >> 4) & 7u, r = ((0u - a1l) >> 2) & 3u;
+  const uint32_t jt = (topl >> 4) & 7u, ht = 4u - ((topl >> 2) & 3u);
+  uint32_t tab = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t jk = (j_last - k) & 7u;
+    tab |= (jk < jt ? kHeadZero : (jk == jt ? ht : 0u)) << (3u * k);
+  }
+  const uint32_t v = (uint32_t)(ax >> kRecVShift) & 3u, z = (uint32_t)(ax >> kRecZShift) & 3u;
+  const uint32_t m = v | (z << 3) | (r << 5);  // meta bits 3..9
+  const uint64_t L = (((a1 - 1u) & ~127ull) - 128ull * (ns - 1u)) & kRecAddrMask;
+  X = L | ((uint64_t)(j_last | ((ns - lines) << 3) | (m << 7)) << kPkWShift);
+  Y = tab | (((uint32_t)(ax >> kJobLidShift) & 255u) << kPkIdShift);
+}
+static_assert(kPkJlShift == kPkWShift - 32 && kPkXShift == kPkJlShift + 3 && kPkMetaShift == kPkXShift + 4,
+              "format B fields");
+
+// A fast round's per-lane state from its format-A record.
+__device__ __forceinline__ RaggedRound fast_round_decode(uint32_t Y, const LaneConsts& c, uint32_t hw) {
+  RaggedRound rr;
+  rr.hw = hw;
+  rr.cb = 0;  // no fallback chunks in a fast round
+  rr.top_slot = (int32_t)((Y >> kPkTopShift) & 15u);
+  rr.meta = ((Y >> kPkKtShift) & 7u) == c.k ? Y : (Y & ~kMetaHeadMask);  // bits above 12: not meta fields
+  rr.id = Y >> kPkIdShift;
+  return rr;
+}
+__device__ __forceinline__ PairPlan fast_plan_decode(uint64_t X0, uint64_t X1, uint32_t dma_off) {
+  auto one = [&](uint64_t X, uint64_t& db) -> int32_t {
+    db = (X & kRecAddrMask) + dma_off;
+    return (int32_t)(((uint32_t)(X >> 32) - (dma_off << 16)) >> 24);  // (W - dma_off) >> 8, W >= 240 >= dma_off
+  };
+  PairPlan pl;
+  pl.p0 = one(X0, pl.db0);
+  pl.p1 = one(X1, pl.db1);
+  return pl;
+}
+
+// A line round's per-lane state from its format-B record: the head code of lane k from the
+// table, the skip mask (lanes past E16 all 4 streams; lane 0 the words past a1).
+__device__ __forceinline__ RaggedRound line_round_decode(uint64_t X, uint32_t Y, const LaneConsts& c, uint32_t hw) {
+  const uint32_t xh = (uint32_t)(X >> 32);
   RaggedRound rr;
   rr.hw = hw;
   rr.cb = 0;  // no fallback chunks in a line round
-  rr.top_slot = rr.ns() - (int32_t)lines;
-  const uint32_t j_last = ((a1l - 1u) >> 4) & 7u, r = ((0u - a1l) >> 2) & 3u;
-  const uint32_t jk = (j_last - c.k) & 7u, jt = (topl >> 4) & 7u, wt = (topl >> 2) & 3u;
-  const uint32_t head = jk < jt ? kHeadZero : (jk == jt ? 4u - wt : 0u);
-  const uint32_t skip = c.k > j_last ? 0xFu : (c.k == 0u ? (0xF0u >> r) & 0xFu : 0u);
-  const uint32_t v = (uint32_t)(ax >> kRecVShift) & 3u, z = (uint32_t)(ax >> kRecZShift) & 3u;
-  rr.meta = head | (v << kMetaVShift) | (z << kMetaNTailShift) | kMetaStore | (r << kMetaLineRShift) |
-            (skip << kMetaSkipShift);
-  rr.id = id;
+  rr.top_slot = (int32_t)((xh >> kPkXShift) & 15u);
+  const uint32_t j_last = (xh >> kPkJlShift) & 7u, r = (xh >> (kPkMetaShift + 5)) & 3u;
+  const uint32_t head = (Y >> (3u * c.k)) & 7u;
+  const uint32_t skip = (c.k > j_last ? 0xFu : 0u) | (c.k == 0u ? (0xF0u >> r) & 0xFu : 0u);
+  rr.meta = head | ((xh >> (kPkMetaShift - 3)) & 0x3F8u) | kMetaStore | (skip << kMetaSkipShift);
+  rr.id = Y >> kPkIdShift;
   return rr;
 }
-
 // The DMA plan of a line round: for each DMA packet, the lane's 16 B of pair 0 (half h of the
 // pair: the line NS - 1 - h lines before the last one; chunk (p + j_last + 1) mod 8 of it) and
 // the first pair whose line of half h is one of the packet's (earlier ones: the zero chunk).
-__device__ __forceinline__ PairPlan line_pair_plan(uint64_t ax0, uint32_t info0, uint64_t ax1, uint32_t info1,
-                                                   int32_t ns, uint32_t lane) {
-  const uint32_t h = ((lane >> 3) ^ (lane >> 4)) & 1u, p = lane & 7u;
-  auto one = [&](uint64_t ax, uint32_t info, uint64_t& db) -> int32_t {
-    const uint64_t a1 = ax & kRecAddrMask;
-    const uint32_t a1l = (uint32_t)a1, nsteps = info & kRecStepsMask, pad = (info >> kRecPadShift) << 2;
-    const uint32_t topl = a1l - (128u * nsteps - pad);
-    const int32_t lines = (int32_t)((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) + 1;
-    db = ((a1 - 1u) & ~127ull) - 128u * (uint64_t)(ns - 1 - (int32_t)h) + 16u * ((p + ((a1l - 1u) >> 4) + 1u) & 7u);
-    const int32_t x = ns - lines - (int32_t)h;  // slot of the first line, minus h
-    return x > 0 ? (x + 1) >> 1 : 0;
+__device__ __forceinline__ PairPlan line_plan_decode(uint64_t X0, uint64_t X1, uint32_t dma_off) {
+  const uint32_t h128 = dma_off & 128u, p16 = (dma_off & 0x70u) + 16u;  // 128 h, 16 (p + 1)
+  auto one = [&](uint64_t X, uint64_t& db) -> int32_t {
+    const uint32_t xh = (uint32_t)(X >> 32);
+    db = (X & kRecAddrMask) + (h128 | ((p16 + 16u * ((xh >> kPkJlShift) & 7u)) & 0x70u));
+    const int32_t x = (int32_t)((xh >> kPkXShift) & 15u);
+    return max(0, (x - (int32_t)(h128 >> 7) + 1) >> 1);
   };
   PairPlan pl;
-  pl.p0 = one(ax0, info0, pl.db0);
-  pl.p1 = one(ax1, info1, pl.db1);
+  pl.p0 = one(X0, pl.db0);
+  pl.p1 = one(X1, pl.db1);
   return pl;
 }
 
@@ -1984,7 +2059,6 @@ constexpr int kJobAhead = 2;                                     // jobs built a
 static_assert(kJobSlots >= (2 * kWavesPerBlock - 1) / kMinJobRounds + kJobAhead + 1, "prologue jobs need their slots");
 constexpr uint32_t kJobRoundBytes = 96;                          // per round: u64 ax[8], u32 info[8]
 constexpr uint32_t kJobRecBytes = kJobRounds * kJobRoundBytes;   // 3 KiB, also the descriptor staging
-constexpr int kJobLidShift = 54;                                 // local id (0..255) in ax bits 54..61
 constexpr uint32_t kJobClassWords = 6;                           // 17 classes (16 = no packet), 3 x 10 bits
 constexpr uint32_t kJobSpinLimit = 1u << 22;                     // give up rather than hang (never hit)
 // Failure bits (g_fault_word, enet_crc_device_status): which wait gave up first in a wave.
@@ -2233,15 +2307,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     }
 #pragma unroll
     for (uint32_t w = 0; w < kJobClassWords; ++w) start[w] = start[w] - cnt[w] + base[w];
+    uint32_t qpos[4];  // each packet's position in the job's sorted order
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       uint32_t sw = 0;
 #pragma unroll
       for (uint32_t w = 0; w < kJobClassWords; ++w) sw = cls[i] / 3u == w ? start[w] : sw;
       const uint32_t q = ((sw >> (10u * (cls[i] % 3u))) & 1023u) + rank[i];
-      const uint32_t r = st + (q >> 3) * kJobRoundBytes;
-      lds_st64(r + 8u * (q & 7u), ax[i]);
-      lds_st32(r + 64u + 4u * (q & 7u), info[i]);
+      qpos[i] = q;
       if (cls[i] < (uint32_t)kStepClasses) {  // a valid packet: the round header
         const uint32_t h = hdr + 16u * (q >> 3), ns_i = info[i] & kRecStepsMask;
         asm volatile("ds_max_u32 %0, %1\n\tds_min_u32 %0, %1 offset:4" : : "v"(h), "v"(ns_i) : "memory");
@@ -2264,9 +2337,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const int32_t lim = two_pairs ? ns : B + 1;
       const bool partial = (lane + 1u) * kPacketsPerWave > n;
       const bool near = (hv.z & 1u) != 0u;
-      const bool fast = !near && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)hv.y <= (int64_t)lim &&
+      // mx > 0: a round of empty packets only (B = 4) has no fast body (pair_round_short: B <= 3).
+      const bool fast = !near && mx > 0 && ns <= kRaggedFastMax && (int64_t)ns - (int64_t)hv.y <= (int64_t)lim &&
                         (!partial || two_pairs);
-      // A line round (line_round_from_record): 8 packets of one step count n in kLineMinSteps ..
+      // A line round (format B, pack_line): 8 packets of one step count n in kLineMinSteps ..
       // 13, none near the caller's base.  They span n or n + 1 lines (n + 1 for some: header
       // bit 1); NS = that maximum rounded up to even, first lines in slots B .. B + 1.
       // Only when that costs no slot over the end-anchored round (an even n with a packet of
@@ -2276,6 +2350,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const uint32_t word = line ? (uint32_t)nl | ((uint32_t)(nl - ml) << 26) | ((hv.z & 4u) << 27) | 0xC0000000u
                                  : (uint32_t)ns | ((uint32_t)B << 26) | (fast ? 0x80000000u : 0u);
       lds_st32(hdr + 16u * lane + 12u, word);
+    }
+    // The records at their sorted positions: packed for fast and line rounds (this wave's
+    // header words above are written before its reads below), raw for the others.
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t q = qpos[i], r = st + (q >> 3) * kJobRoundBytes;
+      const uint32_t hw = lds_ld32(hdr + 16u * (q >> 3) + 12u);
+      uint64_t X = ax[i];
+      uint32_t Y = info[i];
+      if ((hw >> 30) & 1u)
+        pack_line(ax[i], info[i], hw & 0x3FFFFFFu, X, Y);
+      else if ((int32_t)hw < 0)
+        pack_fast(ax[i], info[i], cls[i] < (uint32_t)kStepClasses, hw & 0x3FFFFFFu, X, Y);
+      lds_st64(r + 8u * (q & 7u), X);
+      lds_st32(r + 64u + 4u * (q & 7u), Y);
     }
     if (lane == 0) lds_st32((ENET_S_OFF(ready) + 4u * slot), gen);
   };
@@ -2337,9 +2426,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // Rounds holding a packet near the caller's base (the batch's first few) take their own copy
     // of the decode: the others carry no near-base code at all (one scalar branch).
     RaggedRound rr;
-    if ((hw >> 30) & 1u) {  // a line round (never near the base, never partial)
-      rr = line_round_from_record(ax, info, (uint32_t)(ax >> kJobLidShift) & 255u, c, hw);
-      rr.plan = line_pair_plan(ax0, (uint32_t)infod, ax1, (uint32_t)(infod >> 32), ns, lane);
+    if ((hw >> 30) & 1u) {  // a line round (never near the base, never partial): format B
+      rr = line_round_decode(ax, info, c, hw);
+      rr.plan = line_plan_decode(ax0, ax1, dma_off);
+    } else if ((int32_t)hw < 0) {  // a fast round (never near the base): format A
+      rr = fast_round_decode(info, c, hw);
+      rr.plan = fast_plan_decode(ax0, ax1, dma_off);
     } else if (near_round) {
       rr = pair_round_from_record(ax, info, rv && ((ax >> kRecValidBit) & 1u), (uint32_t)(ax >> kJobLidShift) & 255u,
                                   c, hw, true);
@@ -2384,7 +2476,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
       const uint64_t J0 = job_of(k0);
       const uint32_t n0 = job_count(J0);
       const u32x4 v = lds_ld128((job_off(slot0) + (uint32_t)offsetof(JobSlot, res)) + 16u * lane);
-      uint32_t* dst = out + J0 * JP + 4u * lane;
+      // The lane's offset through an asm statement: hipcc would hoist the lane's output pointer
+      // out of the round loop and spill it (a scratch reload per job).
+      uint32_t l16;
+      asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(l16) : "v"(lane));
+      uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(out + J0 * JP) + l16);
       if (4u * lane + 4u <= n0) {
         reinterpret_cast<U32x4A4*>(dst)->v = v;
       } else {
@@ -2445,8 +2541,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     // rounds; no fallback chunk; NS <= kRaggedFastMax) take an unrolled body per NS, mixed-class
     // rounds included (round 4: 149.5 vs 157.8 us on G2); the others (fallback
     // chunks near the caller's base, longer or wider-spread rounds) the generic loop.
-    if (!cur.fast() || !pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
-                                          std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{}))
+    // A fast round always has its body (its NS and B are those the header rule admits; the
+    // record is packed for it, so the generic loop could not run it).
+    if (cur.fast())
+      (void)pair_round_dispatch(cur, cur.plan, nxt.plan, R, c, h0, h1, h2, h3,
+                                std::make_integer_sequence<int, (kRaggedFastMax - kPairMinSlots) / 2>{});
+    else
       pair_round_generic(cur, cur.plan, nxt.plan, R, c, lds, h0, h1, h2, h3);
     if (cur.line() && cur.line_rot()) line_rotate(cur.meta, lane, h0, h1, h2, h3);  // this lane's a1-grid streams
     uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams

@@ -316,6 +316,20 @@ def test_ragged_region_sort_edges(dev, count):
     assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
 
 
+@pytest.mark.parametrize("zero_frac", [0.08, 0.3])
+def test_ragged_empty_rounds(dev, zero_frac):
+    # Jobs whose first rounds hold only empty packets (no fast body: the generic loop), next to
+    # fast, line and generic rounds (packed and raw records); 64 of them in one batch.
+    count = 64 * 136 + 5
+    rng = np.random.default_rng(int(zero_frac * 100))
+    lengths = rng.choice(np.array([0, 1, 100, 700, 1100, 1392, 1800, 2500, 3000], dtype=np.uint32), size=count)
+    lengths[rng.random(count) < zero_frac] = 0
+    lengths[:40] = 0
+    offsets = (packed_offsets(lengths) + np.cumsum(rng.integers(0, 3, size=count))).astype(np.uint64)
+    data = splitmix64_bytes(count + 7, int(offsets[-1] + lengths[-1]) + 8)
+    assert np.array_equal(ragged_on_device(data, offsets, lengths, dev), _oracle.crc32_ragged(data, offsets, lengths))
+
+
 @pytest.mark.parametrize("shape", ["near_base", "wide_spread", "tiny", "long_mix", "mtu_unaligned", "one_job"])
 def test_ragged_round_paths(dev, shape):
     """The round bodies of crc32_ragged_jobs_kernel (8 packets per round, 128-B steps; first

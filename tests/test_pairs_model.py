@@ -74,7 +74,7 @@ def simulate_round(mem, base4, packets, valid, rng_dummy=None):
     B = ns - mx
     lim = MIN_SLOTS if ns == MIN_SLOTS else B + 1
     partial = not all(valid)
-    fast = (not near_round) and ns <= 14 and ns - mn <= lim and (not partial or ns == MIN_SLOTS)
+    fast = (not near_round) and mx > 0 and ns <= 14 and ns - mn <= lim and (not partial or ns == MIN_SLOTS)
     if fast:
         for P in range(2, ns // 2):
             for i in range(2):
