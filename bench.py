@@ -801,6 +801,19 @@ def parse_args(argv):
     return ap.parse_args(argv)
 
 
+def _with_stdout_on_stderr(fn):
+    """fn() with file descriptor 1 redirected to descriptor 2 (C-level prints included)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        return fn()
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
@@ -824,7 +837,14 @@ def main(argv=None) -> int:
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")  # timing reduction only; no data-path collective
+        # Timing reduction only; no data-path collective.  The gloo transport prints its
+        # connection messages on stdout (file descriptor 1), where the driver reads rank 0's one
+        # JSON line: the init and a first barrier run with descriptor 1 pointed at stderr.
+        def _init():
+            dist.init_process_group("gloo")
+            dist.barrier()
+
+        _with_stdout_on_stderr(_init)
     shared = os.environ.get("BENCH_SHARE_GPUS") == "1" and torch.cuda.device_count() < world
     dev = torch.device("cuda", local % torch.cuda.device_count() if shared else local)
     torch.cuda.set_device(dev)

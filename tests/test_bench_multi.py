@@ -15,9 +15,6 @@ REPO = os.path.dirname(HERE)
 
 
 def _rank(rank: int, world: int, port: int, outdir: str) -> None:
-    import contextlib
-    import io
-
     sys.path.insert(0, REPO)
     import torch
 
@@ -47,11 +44,23 @@ def _rank(rank: int, world: int, port: int, outdir: str) -> None:
     bench.open_ceiling = lambda dev: None  # the read-ceiling probe needs a GPU
     bench.time_steps = time_steps
     bench.device_record = lambda dev, r: {"rank": r, "device": dev.index, "pci": f"0000:{0x10 * (r + 1):02x}:00"}
-    buf = io.StringIO()
-    with contextlib.redirect_stdout(buf):
-        rc = bench.main(["--gpus", str(world), "--steps", "4", "--warmup", "1", "--cpu-seconds", "0"])
+    # Descriptor-level capture: whatever reaches file descriptor 1 (C-level prints such as the
+    # gloo transport's connection messages included) is what the driver would read.
+    path = os.path.join(outdir, f"stdout{rank}.txt")
+    sys.stdout.flush()
+    saved = os.dup(1)
+    with open(path, "w") as cap:
+        os.dup2(cap.fileno(), 1)
+        try:
+            rc = bench.main(["--gpus", str(world), "--steps", "4", "--warmup", "1", "--cpu-seconds", "0"])
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+    with open(path) as f:
+        text = f.read()
     with open(os.path.join(outdir, f"rank{rank}.txt"), "w") as f:
-        f.write(f"{rc}\n{buf.getvalue()}")
+        f.write(f"{rc}\n{text}")
 
 
 def test_multi_gpu_line_shape(tmp_path):
@@ -65,7 +74,8 @@ def test_multi_gpu_line_shape(tmp_path):
     rc0, out0 = (tmp_path / "rank0.txt").read_text().split("\n", 1)
     rc1, out1 = (tmp_path / "rank1.txt").read_text().split("\n", 1)
     assert rc0 == "0" and rc1 == "0" and out1.strip() == ""
-    line = json.loads(out0.strip().splitlines()[-1])
+    assert len(out0.strip().splitlines()) == 1, out0  # rank 0's stdout: exactly the JSON line
+    line = json.loads(out0.strip())
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["packets_per_gpu"] == 2 << 20  # configs[3]: 16M over 8
     # main line: max over ranks (rank 1 is twice as slow)
