@@ -36,7 +36,9 @@ def draw(rng):
     else:  # long tail up to 8 KiB
         lengths = np.minimum(rng.exponential(700, size=n).astype(np.int64), 8192)
     lengths = np.clip(lengths, 0, None).astype(np.uint32)
-    lengths[rng.random(n) < 0.02] = 0
+    # zero-length packets: 2 % as a rule, 25 % in some batches (jobs whose first rounds hold only
+    # empty packets: no fast body, the generic loop)
+    lengths[rng.random(n) < (0.25 if rng.random() < 0.2 else 0.02)] = 0
     gaps = rng.integers(0, 8, size=n) if rng.random() < 0.5 else np.zeros(n, np.int64)
     starts = np.concatenate([[0], np.cumsum(lengths.astype(np.int64) + gaps)[:-1]])
     if rng.random() < 0.2:  # some packets re-read earlier bytes (overlaps are allowed)

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: randomized ragged batches through the product (line rounds on) against the oracle,
-# with a new seed.
+# Round 6: randomized ragged batches through the product against the oracle, with a new seed.
+#   gpurun -- bash scripts/gpu_r06_fuzz.sh <tag> [seed]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-r06_fuzz}
