@@ -1736,12 +1736,14 @@ __device__ __forceinline__ void pack_line(uint64_t ax, uint32_t info, uint32_t n
   const uint32_t lines = ((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) + 1u;
   const uint32_t j_last = ((a1l - 1u) >> 4) & 7u, r = ((0u - a1l) >> 2) & 3u;
   const uint32_t jt = (topl >> 4) & 7u, ht = 4u - ((topl >> 2) & 3u);
-  uint32_t tab = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t jk = (j_last - k) & 7u;
-    tab |= (jk < jt ? kHeadZero : (jk == jt ? ht : 0u)) << (3u * k);
-  }
+  // Entry k is the code of chunk jk = (j_last - k) mod 8: kHeadZero for jk < jt, ht for jk = jt,
+  // else 0.  Indexed by m = 7 - jk that is kHeadZero in the fields m >= 8 - jt and ht in field
+  // 7 - jt; entry k is field (k + 7 - j_last) mod 8 of it, a rotation of the 24-bit word.
+  // (The loop over k cost 45 VALU per packet; host model: tests/test_packed_records_model.py.)
+  constexpr uint32_t kZeroRep = kHeadZero * 0x249249u;  // kHeadZero in all 8 fields
+  const uint32_t rev = (kZeroRep & (0xFFFFFFu << (3u * (8u - jt)))) | (ht << (3u * (7u - jt)));
+  const uint32_t rot = 3u * (7u - j_last);
+  const uint32_t tab = ((rev >> rot) | (rev << (24u - rot))) & 0xFFFFFFu;
   const uint32_t v = (uint32_t)(ax >> kRecVShift) & 3u, z = (uint32_t)(ax >> kRecZShift) & 3u;
   const uint32_t m = v | (z << 3) | (r << 5);  // meta bits 3..9
   const uint64_t L = (((a1 - 1u) & ~127ull) - 128ull * (ns - 1u)) & kRecAddrMask;
@@ -2059,13 +2061,14 @@ constexpr int kJobAhead = 2;                                     // jobs built a
 static_assert(kJobSlots >= (2 * kWavesPerBlock - 1) / kMinJobRounds + kJobAhead + 1, "prologue jobs need their slots");
 constexpr uint32_t kJobRoundBytes = 96;                          // per round: u64 ax[8], u32 info[8]
 constexpr uint32_t kJobRecBytes = kJobRounds * kJobRoundBytes;   // 3 KiB, also the descriptor staging
-constexpr uint32_t kJobClassWords = 6;                           // 17 classes (16 = no packet), 3 x 10 bits
+constexpr uint32_t kJobClassWords = 4;                           // 16 classes, 4 x 8 bits (no packet: not counted)
 constexpr uint32_t kJobSpinLimit = 1u << 22;                     // give up rather than hang (never hit)
 // Failure bits (g_fault_word, enet_crc_device_status): which wait gave up first in a wave.
 constexpr uint32_t kFaultReady = 1u;     // a job's records never became ready
 constexpr uint32_t kFaultConsumed = 2u;  // a job slot's previous job was never fully read
 constexpr uint32_t kFaultFreed = 4u;     // a result slot's previous job was never flushed
 static_assert(kJobPackets == 4 * 64, "4 packets per lane");
+static_assert(kStepClasses == 4 * (int)kJobClassWords && kJobPackets <= 256, "job_build: 8-bit class fields, 4 per word");
 static_assert(kJobRecBytes == kJobPackets * 12, "staging: u64 offsets + u32 lengths");
 
 struct JobSlot {
@@ -2129,9 +2132,6 @@ __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) {
 }
 __device__ __forceinline__ void lds_st32_nowait(uint32_t a, uint32_t v) {
   asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_st64(uint32_t a, uint64_t v) {
-  asm volatile("ds_write_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : : "v"(a), "v"(v) : "memory");
 }
 __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t a, uint32_t v) {
   uint32_t old;
@@ -2264,8 +2264,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   auto job_build = [&](uint64_t J, uint32_t slot, uint32_t gen) {
     asm volatile("s_waitcnt vmcnt(%0)" : : "i"(kDescWait) : "memory");
     const uint32_t st = (job_off(slot) + (uint32_t)offsetof(JobSlot, rec));
-    const u32x4 o01 = lds_ld128(st + 32u * lane), o23 = lds_ld128(st + 32u * lane + 16u);
-    const u32x4 ln = lds_ld128(st + 2048u + 16u * lane);
+    u32x4 o01, o23, ln;
+    asm volatile(  // one round trip
+        "ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:16\n\tds_read_b128 %2, %4\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(o01), "=&v"(o23), "=&v"(ln)
+        : "v"(st + 32u * lane), "v"(st + 2048u + 16u * lane)
+        : "memory");
     const uint64_t off[4] = {o01.x | (uint64_t)o01.y << 32, o01.z | (uint64_t)o01.w << 32,
                              o23.x | (uint64_t)o23.y << 32, o23.z | (uint64_t)o23.w << 32};
     const uint32_t len[4] = {ln.x, ln.y, ln.z, ln.w};
@@ -2287,43 +2291,50 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #pragma unroll
       for (int j = 0; j < i; ++j) rank[i] += cls[j] == cls[i] ? 1u : 0u;
     }
-    // Class counts of this lane as 10-bit fields (class c: word c / 3, field c % 3), their
-    // inclusive scan over the lanes, the job's totals, and each class's first position.
-    uint32_t cnt[kJobClassWords], start[kJobClassWords], base[kJobClassWords];
+    // Class counts of this lane as 8-bit fields (class c: word c / 4, field c % 4; positions past
+    // the job's packets are not counted, they keep their own index), their inclusive scan over the
+    // lanes, the job's totals, and each class's first position, all in wrapping 32-bit words.  A
+    // field reaches 256, or a sum of fields carries into the next field, only when every packet of
+    // the job lies in that class or below: the carry lands in classes that hold no packet
+    // (tests/test_job_sort_model.py restates this arithmetic and checks every position).
+    uint32_t cnt[kJobClassWords];
+#pragma unroll
+    for (uint32_t w = 0; w < kJobClassWords; ++w) cnt[w] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t one = cls[i] < (uint32_t)kStepClasses ? 1u << (8u * (cls[i] & 3u)) : 0u;
+#pragma unroll
+      for (uint32_t w = 0; w < kJobClassWords; ++w) cnt[w] += (cls[i] >> 2) == w ? one : 0u;
+    }
+    uint32_t start[kJobClassWords];
+    uint32_t run = 0;  // packets of the classes below word w (mod 256)
 #pragma unroll
     for (uint32_t w = 0; w < kJobClassWords; ++w) {
-      cnt[w] = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) cnt[w] += cls[i] / 3u == w ? 1u << (10u * (cls[i] % 3u)) : 0u;
       start[w] = wave_inclusive_add(cnt[w]);
-      base[w] = 0;
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)start[w], 63);
+      // field f: run + the totals of fields 0 .. f - 1 (tot x 0x01010100 sums the fields below)
+      const uint32_t base = tot * 0x01010100u + (run & 255u) * 0x01010101u;
+      run += (tot * 0x01010101u) >> 24;
+      start[w] = start[w] - cnt[w] + base;
     }
-    uint32_t run = 0;
-#pragma unroll
-    for (uint32_t cl = 0; cl <= (uint32_t)kStepClasses; ++cl) {
-      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)start[cl / 3u], 63);
-      base[cl / 3u] |= run << (10u * (cl % 3u));
-      run += (tot >> (10u * (cl % 3u))) & 1023u;
-    }
-#pragma unroll
-    for (uint32_t w = 0; w < kJobClassWords; ++w) start[w] = start[w] - cnt[w] + base[w];
     uint32_t qpos[4];  // each packet's position in the job's sorted order
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      uint32_t sw = 0;
-#pragma unroll
-      for (uint32_t w = 0; w < kJobClassWords; ++w) sw = cls[i] / 3u == w ? start[w] : sw;
-      const uint32_t q = ((sw >> (10u * (cls[i] % 3u))) & 1023u) + rank[i];
+      const uint32_t cw = cls[i] >> 2;
+      const uint32_t sw = cw & 2u ? (cw & 1u ? start[3] : start[2]) : (cw & 1u ? start[1] : start[0]);
+      const bool valid = cls[i] < (uint32_t)kStepClasses;
+      const uint32_t q = valid ? ((sw >> (8u * (cls[i] & 3u))) & 255u) + rank[i] : 4u * lane + (uint32_t)i;
       qpos[i] = q;
-      if (cls[i] < (uint32_t)kStepClasses) {  // a valid packet: the round header
+      if (valid) {  // the round header
         const uint32_t h = hdr + 16u * (q >> 3), ns_i = info[i] & kRecStepsMask;
         asm volatile("ds_max_u32 %0, %1\n\tds_min_u32 %0, %1 offset:4" : : "v"(h), "v"(ns_i) : "memory");
-        if ((ax[i] >> kRecNearBit) & 1u) lds_or_nowait(h + 8u, 1u);
-        // bit 1: the packet spans nsteps + 1 lines (a line round then needs one slot more)
+        // bit 0: near the caller's base; bit 1: the packet spans nsteps + 1 lines (a line round
+        // then needs one slot more); bit 2: its a1 is off the 16-B grid (line_rotate)
         const uint32_t a1l = (uint32_t)ax[i], topl = a1l - (128u * ns_i - ((info[i] >> kRecPadShift) << 2));
-        if (((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) == ns_i) lds_or_nowait(h + 8u, 2u);
-        // bit 2: its a1 is not on the 16-B grid (a line round then exchanges words, line_rotate)
-        if ((a1l & 12u)) lds_or_nowait(h + 8u, 4u);
+        const uint32_t flags = ((uint32_t)(ax[i] >> kRecNearBit) & 1u) |
+                               (((((a1l - 1u) >> 7) - (topl >> 7)) & 0x1FFFFFFu) == ns_i ? 2u : 0u) |
+                               (a1l & 12u ? 4u : 0u);
+        if (flags) lds_or_nowait(h + 8u, flags);
       }
     }
     // Per round, make_round's rule evaluated once here: hdr.w = ns | B << 26 | fast << 31 (the
@@ -2353,18 +2364,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     }
     // The records at their sorted positions: packed for fast and line rounds (this wave's
     // header words above are written before its reads below), raw for the others.
+    uint32_t hwq[4];  // the header words of the packets' rounds, one round trip
+    asm volatile(
+        "ds_read_b32 %0, %4 offset:12\n\tds_read_b32 %1, %5 offset:12\n\t"
+        "ds_read_b32 %2, %6 offset:12\n\tds_read_b32 %3, %7 offset:12\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(hwq[0]), "=&v"(hwq[1]), "=&v"(hwq[2]), "=&v"(hwq[3])
+        : "v"(hdr + 16u * (qpos[0] >> 3)), "v"(hdr + 16u * (qpos[1] >> 3)), "v"(hdr + 16u * (qpos[2] >> 3)),
+          "v"(hdr + 16u * (qpos[3] >> 3))
+        : "memory");
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t q = qpos[i], r = st + (q >> 3) * kJobRoundBytes;
-      const uint32_t hw = lds_ld32(hdr + 16u * (q >> 3) + 12u);
+      const uint32_t q = qpos[i], r = st + (q >> 3) * kJobRoundBytes, hw = hwq[i];
       uint64_t X = ax[i];
       uint32_t Y = info[i];
       if ((hw >> 30) & 1u)
         pack_line(ax[i], info[i], hw & 0x3FFFFFFu, X, Y);
       else if ((int32_t)hw < 0)
         pack_fast(ax[i], info[i], cls[i] < (uint32_t)kStepClasses, hw & 0x3FFFFFFu, X, Y);
-      lds_st64(r + 8u * (q & 7u), X);
-      lds_st32(r + 64u + 4u * (q & 7u), Y);
+      // not waited for: the ready flag below is written after them (LDS operations of a wave
+      // complete in order), and its store waits
+      asm volatile("ds_write_b64 %0, %1\n\tds_write_b32 %2, %3" : : "v"(r + 8u * (q & 7u)), "v"(X),
+                   "v"(r + 64u + 4u * (q & 7u)), "v"(Y) : "memory");
     }
     if (lane == 0) lds_st32((ENET_S_OFF(ready) + 4u * slot), gen);
   };

@@ -134,6 +134,30 @@ def pack_fast(ax, info, valid, ns):
     return X, Y
 
 
+def head_table_loop(j_last, jt, ht):
+    """Format B's head table by its definition: entry k is the code of chunk (j_last - k) mod 8."""
+    tab = 0
+    for k in range(8):
+        jk = (j_last - k) & 7
+        tab |= (HEAD_ZERO if jk < jt else (ht if jk == jt else 0)) << (3 * k)
+    return tab
+
+
+def head_table(j_last, jt, ht):
+    """pack_line's closed form: the fields m = 7 - jk, then a 24-bit rotation."""
+    rep = HEAD_ZERO * 0x249249
+    rev = (rep & u32(0xFFFFFF << (3 * (8 - jt)))) | (ht << (3 * (7 - jt)))
+    rot = 3 * (7 - j_last)
+    return ((rev >> rot) | u32(rev << (24 - rot))) & 0xFFFFFF
+
+
+def test_head_table_closed_form():
+    for j_last in range(8):
+        for jt in range(8):
+            for ht in range(1, 5):
+                assert head_table(j_last, jt, ht) == head_table_loop(j_last, jt, ht), (j_last, jt, ht)
+
+
 def pack_line(ax, info, ns):
     f = fields(ax, info)
     a1 = f["a1"]
@@ -142,10 +166,8 @@ def pack_line(ax, info, ns):
     lines = ((((u32(a1l - 1)) >> 7) - (topl >> 7)) & 0x1FFFFFF) + 1
     j_last, r = (u32(a1l - 1) >> 4) & 7, (u32(-a1l) >> 2) & 3
     jt, ht = (topl >> 4) & 7, 4 - ((topl >> 2) & 3)
-    tab = 0
-    for k in range(8):
-        jk = (j_last - k) & 7
-        tab |= (HEAD_ZERO if jk < jt else (ht if jk == jt else 0)) << (3 * k)
+    tab = head_table(j_last, jt, ht)
+    assert tab == head_table_loop(j_last, jt, ht)
     m = f["v"] | f["z"] << 3 | r << 5
     L = (((a1 - 1) & ~127) - 128 * (ns - 1)) & MASK48
     assert 0 <= ns - lines < 16
