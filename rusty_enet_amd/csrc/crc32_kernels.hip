@@ -674,16 +674,20 @@ struct RaggedRecord {
 };
 
 __device__ __forceinline__ RaggedRecord ragged_record(uint64_t sa, uint32_t len, uint64_t base4) {
-  const uint32_t z = len ? (4u - (uint32_t)((sa + len) & 3u)) & 3u : 0u;
-  const PacketGeo g = make_geo(sa, (uint64_t)len + z);  // runs to the next 4-byte boundary
-  const uint32_t nwords = (uint32_t)((g.a1 - g.top) >> 2);
-  const uint32_t pad = 128u * (uint32_t)g.nsteps - 4u * nwords;  // 0..124
-  const uint64_t near = g.top - base4 < 16 ? 1ull : 0ull;
+  // make_geo(sa, len + z) in 32-bit words where the values allow it: v + len + z is a multiple
+  // of 4 (0 for an empty packet), so nwords = (v + len + z) / 4 without a 64-bit subtraction.
+  const uint32_t v = (uint32_t)sa & 3u;
+  const uint32_t z = len ? (4u - (((uint32_t)sa + len) & 3u)) & 3u : 0u;
+  const uint32_t nwords = (len >> 2) + (((len & 3u) + v + z) >> 2);
+  const uint32_t nsteps = (((nwords + 3u) >> 2) + (uint32_t)kLanesPerPacket - 1u) / (uint32_t)kLanesPerPacket;
+  const uint32_t pad = 128u * nsteps - 4u * nwords;  // 0..124
+  const uint64_t top = sa & ~(uint64_t)3, a1 = top + 4ull * nwords;
+  const uint64_t near = top - base4 < 16 ? 1ull : 0ull;
   RaggedRecord r;
-  r.ax = g.a1 | ((sa & 3u) << kRecVShift) | ((uint64_t)z << kRecZShift) | (near << kRecNearBit) |
+  r.ax = a1 | ((uint64_t)v << kRecVShift) | ((uint64_t)z << kRecZShift) | (near << kRecNearBit) |
          (1ull << kRecValidBit);
-  r.info = (uint32_t)g.nsteps | ((pad >> 2) << kRecPadShift);
-  r.nsteps = (uint32_t)g.nsteps;
+  r.info = nsteps | ((pad >> 2) << kRecPadShift);
+  r.nsteps = nsteps;
   return r;
 }
 
@@ -2301,10 +2305,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
 #pragma unroll
     for (uint32_t w = 0; w < kJobClassWords; ++w) cnt[w] = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t one = cls[i] < (uint32_t)kStepClasses ? 1u << (8u * (cls[i] & 3u)) : 0u;
-#pragma unroll
-      for (uint32_t w = 0; w < kJobClassWords; ++w) cnt[w] += (cls[i] >> 2) == w ? one : 0u;
+    for (int i = 0; i < 4; ++i) {  // bit 8 c of the 128-bit count word: one 64-bit shift, two selects
+      const uint64_t one = 1ull << (8u * (cls[i] & 7u));
+      const bool lo = cls[i] < 8u, hi = cls[i] - 8u < 8u;  // classes 0..7 / 8..15 (16: no packet)
+      cnt[0] += lo ? (uint32_t)one : 0u;
+      cnt[1] += lo ? (uint32_t)(one >> 32) : 0u;
+      cnt[2] += hi ? (uint32_t)one : 0u;
+      cnt[3] += hi ? (uint32_t)(one >> 32) : 0u;
     }
     uint32_t start[kJobClassWords];
     uint32_t run = 0;  // packets of the classes below word w (mod 256)

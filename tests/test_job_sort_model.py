@@ -117,3 +117,23 @@ def test_g2_like_jobs():
     rng = random.Random(7)
     for _ in range(50):
         check([min(15, ((rng.randint(64, 1392) + 3) // 4 + 3) // 4 // 8 + 1) for _ in range(256)])
+
+
+def test_record_geometry_in_32_bit_words():
+    """ragged_record's 32-bit nwords / nsteps / a1 equal make_geo's 64-bit ones (crc32_geometry.hpp)
+    for every start phase and lengths up to 2^32 - 1."""
+    rng = random.Random(11)
+    lens = [0, 1, 2, 3, 4, 5, 127, 128, 129, 1392, 65536, (1 << 32) - 1, (1 << 32) - 2, (1 << 32) - 5, (1 << 32) - 6]
+    lens += [rng.randrange(1 << 32) for _ in range(2000)]
+    for ln in lens:
+        for sa in (0x7F0000000000 + p for p in range(4)):
+            z = (4 - (sa + ln) % 4) % 4 if ln else 0
+            ea = sa + ln + z
+            top, a1 = sa & ~3, ea & ~3
+            nwords = (a1 - top) >> 2
+            nsteps = ((nwords + 3) // 4 + 7) // 8
+            v = sa & 3
+            nw32 = ((ln >> 2) + (((ln & 3) + v + z) >> 2)) & M
+            ns32 = ((((nw32 + 3) & M) >> 2) + 7) >> 3
+            assert (nw32, ns32, top + 4 * nw32) == (nwords, nsteps, a1), (ln, sa)
+            assert (128 * ns32 - 4 * nw32) & M == 128 * nsteps - 4 * nwords < 128
