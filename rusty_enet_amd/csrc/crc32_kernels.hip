@@ -211,21 +211,48 @@ __device__ __forceinline__ int32_t wave_max_over_groups(int32_t v) {
 // store, so consecutive lanes write consecutive 16 B (a lane-per-row order had every lane
 // of a ds_write_b128 in the same bank group).  `main` = the Horner operator's level.
 // `set0` / `set1`: the operator levels of the block's two sets.
-__device__ __forceinline__ void fill_replicated(uint32_t* lds, int set0, int set1 = 0) {
-  for (uint32_t x = threadIdx.x; x < kRepDwords / 4; x += kBlock) {
-    const uint32_t i = x / (kRowDwords / 4), d = 4u * (x % (kRowDwords / 4));  // row (byte value), first dword
-    const uint32_t second = d >= kSetM1Bytes / 4 ? 1u : 0u, tab = (d % (kSetM1Bytes / 4)) / kRepCopies;
-    const uint32_t v = g_op_tables.op[second ? set1 : set0][tab][i];
-    reinterpret_cast<u32x4*>(lds)[x] = u32x4{v, v, v, v};
-  }
+// Every thread issues all its table loads before its first LDS store (TableLoads): as a loop of
+// load -> wait -> store, a kernel's start paid one memory latency per iteration, 7 to 10 in a
+// row before its first batch load (round 6).
+constexpr int kRepPieces = kRepDwords / 4 / kBlock;  // 16-B pieces of the replicated block per thread
+static_assert(kRepDwords / 4 % kBlock == 0, "whole pieces per thread");
+template <int NT>
+struct TableLoads {
+  uint32_t rep[kRepPieces];  // one dword per replicated piece
+  uint32_t tree[NT];         // unreplicated sets, one dword per 1024
+};
+__device__ __forceinline__ uint32_t replicated_value(uint32_t x, int set0, int set1) {
+  const uint32_t i = x / (kRowDwords / 4), d = 4u * (x % (kRowDwords / 4));  // row (byte value), first dword
+  const uint32_t second = d >= kSetM1Bytes / 4 ? 1u : 0u, tab = (d % (kSetM1Bytes / 4)) / kRepCopies;
+  return g_op_tables.op[second ? set1 : set0][tab][i];
 }
+// NT unreplicated sets after the block: set l is M32^(4 * 2^l) (level l + 2).
+template <int NT>
+__device__ __forceinline__ TableLoads<NT> load_tables(int set0, int set1) {
+  TableLoads<NT> t;
+#pragma unroll
+  for (int r = 0; r < kRepPieces; ++r) t.rep[r] = replicated_value(threadIdx.x + r * kBlock, set0, set1);
+#pragma unroll
+  for (int r = 0; r < NT; ++r) {
+    const uint32_t x = threadIdx.x + r * kBlock, rem = x & 1023u;
+    t.tree[r] = g_op_tables.op[(x >> 10) + 2][rem >> 8][rem & 255u];
+  }
+  return t;
+}
+template <int NT>
+__device__ __forceinline__ void store_tables(uint32_t* lds, uint32_t tree_dword, const TableLoads<NT>& t) {
+#pragma unroll
+  for (int r = 0; r < kRepPieces; ++r) {
+    const uint32_t v = t.rep[r];
+    reinterpret_cast<u32x4*>(lds)[threadIdx.x + r * kBlock] = u32x4{v, v, v, v};
+  }
+#pragma unroll
+  for (int r = 0; r < NT; ++r) lds[tree_dword + threadIdx.x + r * kBlock] = t.tree[r];
+}
+static_assert(kBlock == 1024, "the unreplicated sets are 1024 dwords: one per thread");
 
 __device__ __forceinline__ void fill_lds(uint32_t* lds) {
-  fill_replicated(lds, kMainLevel);
-  for (int x = threadIdx.x; x < kTreeLevels * 1024; x += kBlock) {
-    const int set = x >> 10, rem = x & 1023;  // set l: M32^(4 * 2^l)
-    lds[kTreeDword + x] = g_op_tables.op[set + 2][rem >> 8][rem & 255];
-  }
+  store_tables<kTreeLevels>(lds, kTreeDword, load_tables<kTreeLevels>(kMainLevel, 0));
 }
 
 template <bool kRagged>
@@ -408,11 +435,27 @@ __device__ __forceinline__ uint32_t combine_tree_rep(const uint32_t* lds, uint32
   return y;
 }
 
-__device__ __forceinline__ void fill_lds_regs(uint32_t* lds) {
-  fill_replicated(lds, kMainLevel);
-  fill_replicated(lds + kTreeRepDword, 2, 3);
-  for (int x = threadIdx.x; x < 1024; x += kBlock) lds[kTree16Dword + x] = g_op_tables.op[4][x >> 8][x & 255];
+// The register kernels' tables: the main block, the replicated tree block (M32^4 and M32^8)
+// and the unreplicated M32^16 set; every load issued before any store (TableLoads).  Split in
+// two so that a kernel can issue its first batch loads between them.
+struct RegsTableLoads {
+  TableLoads<0> main, tree;
+  uint32_t t16;
+};
+__device__ __forceinline__ RegsTableLoads load_regs_tables() {
+  RegsTableLoads t;
+  t.main = load_tables<0>(kMainLevel, 0);
+  t.tree = load_tables<0>(2, 3);
+  const uint32_t x = threadIdx.x;
+  t.t16 = g_op_tables.op[4][x >> 8][x & 255u];
+  return t;
 }
+__device__ __forceinline__ void store_regs_tables(uint32_t* lds, const RegsTableLoads& t) {
+  store_tables<0>(lds, 0, t.main);
+  store_tables<0>(lds + kTreeRepDword, 0, t.tree);
+  lds[kTree16Dword + threadIdx.x] = t.t16;
+}
+__device__ __forceinline__ void fill_lds_regs(uint32_t* lds) { store_regs_tables(lds, load_regs_tables()); }
 
 // The packet's register (before trailing bytes), valid on lane k == 0 of the group.
 __device__ __forceinline__ uint32_t combine_streams(const uint32_t* lds, uint32_t h0, uint32_t h1, uint32_t h2,
@@ -1000,11 +1043,7 @@ struct WaveDmaLds {
 static_assert(sizeof(WaveDmaLds) <= 160 * 1024, "LDS");
 
 __device__ __forceinline__ void fill_lds_wave(uint32_t* lds) {
-  fill_replicated(lds, kMainLevel + 3);
-  for (int x = threadIdx.x; x < kWaveTreeLevels * 1024; x += kBlock) {
-    const int set = x >> 10, rem = x & 1023;  // set l: M32^(4 * 2^l)
-    lds[kWaveTreeDword + x] = g_op_tables.op[set + 2][rem >> 8][rem & 255];
-  }
+  store_tables<kWaveTreeLevels>(lds, kWaveTreeDword, load_tables<kWaveTreeLevels>(kMainLevel + 3, 0));
 }
 
 // The packet's register before the shift of its last word (register = M32 y), valid
@@ -1418,9 +1457,11 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
   uint64_t rnd0 = round_of(wv), rnd1 = round_of(wv + kWavesPerBlock);
   u32x4 q[NSL];
   if (threadIdx.x == 0) S.next_dispatch = kWavesPerBlock * 2;
-  fill_lds_regs(lds);
-  __syncthreads();
-  if (rnd0 >= rounds) return;
+  // The table loads, then the first round's line loads (lane_base clamps a round past the
+  // batch), then the table stores: the start pays one memory latency, not the table's and
+  // then the first lines' in a row.
+  const RegsTableLoads tl = load_regs_tables();
+  issue_order_fence();
   {
     const uint64_t lb = lane_base(rnd0);
 #pragma unroll
@@ -1429,6 +1470,9 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
       issue_order_fence();
     }
   }
+  store_regs_tables(lds, tl);
+  __syncthreads();
+  if (rnd0 >= rounds) return;
   uint32_t res = 0, j = 0;
   uint64_t res_round = 0;
   while (rnd0 < rounds) {
@@ -2194,9 +2238,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
     S.next_dispatch = kWavesPerBlock * kLook;
     S.failed = 0;
   }
-  fill_top_masks(S.topmask);
-  fill_lds(lds);
-  __syncthreads();
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2399,9 +2440,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
   // (rounds 0 .. 2 x 16 - 1) and kJobAhead more; the claims of the loop (rounds >= 32)
   // build the rest.  RJ >= 16 (launch_ragged), so that is at most 2 + kJobAhead jobs.
+  // The descriptor DMAs go out before the table fill (its loads are issued after them, and
+  // its wait covers both: one memory latency at the start instead of two in a row).
   const uint32_t first_jobs = (kWavesPerBlock * kLook - 1) / RJ + kJobAhead + 1;
-  if (wv < first_jobs && job_of(wv) < b.njobs) {
-    job_dma(job_of(wv), wv);
+  const bool prologue_job = wv < first_jobs && job_of(wv) < b.njobs;
+  if (prologue_job) job_dma(job_of(wv), wv);
+  fill_top_masks(S.topmask);
+  fill_lds(lds);
+  __syncthreads();
+  if (prologue_job) {
     __builtin_amdgcn_s_waitcnt(0);
     job_build(job_of(wv), wv, wv + 1u);
   }
