@@ -254,6 +254,32 @@ static_assert(kBlock == 1024, "the unreplicated sets are 1024 dwords: one per th
 __device__ __forceinline__ void fill_lds(uint32_t* lds) {
   store_tables<kTreeLevels>(lds, kTreeDword, load_tables<kTreeLevels>(kMainLevel, 0));
 }
+// fill_lds's tables by nt >= 768 threads (t = 0 .. nt - 1 here), all loads before the stores.
+__device__ __forceinline__ void fill_lds_from(uint32_t* lds, uint32_t t, uint32_t nt) {
+  constexpr uint32_t kPieces = kRepDwords / 4, kTree = kTreeLevels * 1024u;
+  constexpr int kRepIt = (kPieces + 767) / 768, kTreeIt = (kTree + 767) / 768;
+  uint32_t rep[kRepIt], tree[kTreeIt];
+#pragma unroll
+  for (int r = 0; r < kRepIt; ++r) {
+    const uint32_t x = t + r * nt;
+    rep[r] = x < kPieces ? replicated_value(x, kMainLevel, 0) : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kTreeIt; ++r) {
+    const uint32_t x = t + r * nt, rem = x & 1023u;
+    tree[r] = x < kTree ? g_op_tables.op[(x >> 10) + 2][rem >> 8][rem & 255u] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kRepIt; ++r) {
+    const uint32_t x = t + r * nt, v = rep[r];
+    if (x < kPieces) reinterpret_cast<u32x4*>(lds)[x] = u32x4{v, v, v, v};
+  }
+#pragma unroll
+  for (int r = 0; r < kTreeIt; ++r) {
+    const uint32_t x = t + r * nt;
+    if (x < kTree) lds[kTreeDword + x] = tree[r];
+  }
+}
 
 template <bool kRagged>
 struct Batch {
@@ -1616,8 +1642,7 @@ __device__ __forceinline__ uint32_t last_word_mask(uint32_t meta, uint32_t k) {
 struct TopMaskEntry {
   u32x4 m, x;
 };
-__device__ __forceinline__ void fill_top_masks(TopMaskEntry* t) {
-  const uint32_t e = threadIdx.x;
+__device__ __forceinline__ void fill_top_masks(TopMaskEntry* t, uint32_t e) {
   if (e >= 32u) return;
   const uint32_t head = e & kMetaHeadMask, v = (e >> kMetaVShift) & 3u;
   uint32_t m[4] = {~0u, ~0u, ~0u, ~0u}, x[4] = {0u, 0u, 0u, 0u};
@@ -2107,6 +2132,7 @@ constexpr int kJobAhead = 2;                                     // jobs built a
 // The prologue builds every job the initial claims (rounds 0 .. 2 x 16 - 1) reach plus kJobAhead
 // more, each into a slot of its own.
 static_assert(kJobSlots >= (2 * kWavesPerBlock - 1) / kMinJobRounds + kJobAhead + 1, "prologue jobs need their slots");
+static_assert(kBlock - 64 * kJobSlots >= 768, "fill_lds_from: the waves that do not build fill the tables");
 constexpr uint32_t kJobRoundBytes = 96;                          // per round: u64 ax[8], u32 info[8]
 constexpr uint32_t kJobRecBytes = kJobRounds * kJobRoundBytes;   // 3 KiB, also the descriptor staging
 constexpr uint32_t kJobClassWords = 4;                           // 16 classes, 4 x 8 bits (no packet: not counted)
@@ -2228,19 +2254,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   __shared__ __attribute__((aligned(16))) RaggedJobsLds S;
   uint32_t* const lds = S.tables;
   constexpr uint32_t kLook = 2;  // a wave knows its current round and the next one
-  if (threadIdx.x < (unsigned)kJobSlots) {
-    S.ready[threadIdx.x] = 0;
-    S.consumed[threadIdx.x] = 0;
-    S.done[threadIdx.x] = 0;
-    S.freed[threadIdx.x] = 0;
-  }
-  if (threadIdx.x == 0) {
-    S.next_dispatch = kWavesPerBlock * kLook;
-    S.failed = 0;
-  }
   const LaneConsts c = lane_consts(b.base);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // Wave w < kJobSlots clears job slot w's flags: the wave that builds into the slot in the
+  // prologue clears them itself, in order before its build sets them.
+  if (wv < (uint32_t)kJobSlots && lane == 0) {
+    S.ready[wv] = 0;
+    S.consumed[wv] = 0;
+    S.done[wv] = 0;
+    S.freed[wv] = 0;
+  }
+  if (threadIdx.x == kBlock - 1) {
+    S.next_dispatch = kWavesPerBlock * kLook;
+    S.failed = 0;
+  }
   if ((uint32_t)(uintptr_t)(LdsVoid*)lds != 0) __builtin_trap();  // horner_step_and_read addresses
 
   auto job_of = [&](uint32_t k) -> uint32_t { return blockIdx.x + k * gridDim.x; };  // < njobs, or >= it past the end
@@ -2440,17 +2468,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((unused)) void crc32_ragged_j
   // Prologue (no ring DMA yet): wave w builds job w, for the jobs of the initial claims
   // (rounds 0 .. 2 x 16 - 1) and kJobAhead more; the claims of the loop (rounds >= 32)
   // build the rest.  RJ >= 16 (launch_ragged), so that is at most 2 + kJobAhead jobs.
-  // The descriptor DMAs go out before the table fill (its loads are issued after them, and
-  // its wait covers both: one memory latency at the start instead of two in a row).
+  // The building waves fetch and sort their jobs while the other waves fill the tables (the
+  // builds do not read the tables): the start is a descriptor fetch plus a build, not a table
+  // fill, a barrier and then a build.
   const uint32_t first_jobs = (kWavesPerBlock * kLook - 1) / RJ + kJobAhead + 1;
-  const bool prologue_job = wv < first_jobs && job_of(wv) < b.njobs;
-  if (prologue_job) job_dma(job_of(wv), wv);
-  fill_top_masks(S.topmask);
-  fill_lds(lds);
-  __syncthreads();
-  if (prologue_job) {
-    __builtin_amdgcn_s_waitcnt(0);
-    job_build(job_of(wv), wv, wv + 1u);
+  if (wv < first_jobs) {
+    if (job_of(wv) < b.njobs) {
+      job_dma(job_of(wv), wv);
+      __builtin_amdgcn_s_waitcnt(0);
+      job_build(job_of(wv), wv, wv + 1u);
+    }
+  } else {
+    const uint32_t t0 = 64u * first_jobs;
+    fill_lds_from(lds, threadIdx.x - t0, kBlock - t0);
+    fill_top_masks(S.topmask, kBlock - 1u - threadIdx.x);
   }
   __syncthreads();
 

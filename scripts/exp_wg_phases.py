@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Experiment (measurement build libenet_crc_amd_wgstamp3.so, profiles/r06/parked/wg_stamps3.patch:
 each workgroup's first wave start, its first wave past the prologue's last barrier, and its last
-wave exit; s_memrealtime at 100 MHz): how long the ragged jobs kernel's start (table fill, the
-first job builds) and its tail take.  Tooling, not product.
+wave exit; s_memrealtime at 100 MHz; the ragged jobs kernel and the whole-line kernel): how long
+a kernel's start (table fill, the first job builds) and its tail take, and whether a workgroup's
+start and end follow its index or its XCD.  Tooling, not product.
 
     ENET_CRC_AMD_LIB=rusty_enet_amd/lib/variants/libenet_crc_amd_wgstamp3.so python scripts/exp_wg_phases.py
 """
@@ -41,12 +42,18 @@ def main() -> int:
         ln = torch.from_numpy(lengths.astype(np.int32)).to(dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         runs[name] = (lambda d=d, off=off, ln=ln, out=out: rea.crc32_batch(d, offsets=off, lengths=ln, out=out))
+    n1 = 1 << 20
+    d1 = torch.randint(0, 256, (n1 * 1200,), dtype=torch.uint8, device=dev, generator=g)
+    out1 = torch.empty(n1, dtype=torch.int32, device=dev)
+    runs["G1"] = lambda: rea.crc32_batch(d1, stride=1200, length=1200, count=n1, out=out1)
     st, mi, en = ((ctypes.c_ulonglong * 4096)() for _ in range(3))
     for name, fn in runs.items():
         for _ in range(30):
             fn()
         torch.cuda.synchronize()
         rows = []
+        starts_acc = np.zeros(cus)
+        ends_acc = np.zeros(cus)
         for _ in range(40):
             assert f(st, mi, en, 4096, 1) == 0
             fn()
@@ -60,7 +67,21 @@ def main() -> int:
             ends = (e - t0) * 0.01
             rows.append((np.median(pro), pro.max(), (s.max() - t0) * 0.01, ends.max(), ends.max() - np.median(ends),
                          np.median(e - m) * 0.01))
+            starts_acc += (s - t0) * 0.01
+            ends_acc += ends
         r = np.array(rows)
+        if name in ("G2", "G1"):
+            sa, ea = starts_acc / 40.0, ends_acc / 40.0
+            idx = np.arange(cus)
+            print(f"{name} per workgroup (mean of 40 launches): corr(blockIdx, start) {np.corrcoef(idx, sa)[0, 1]:.3f}, "
+                  f"corr(blockIdx, end) {np.corrcoef(idx, ea)[0, 1]:.3f}, corr(start, end) {np.corrcoef(sa, ea)[0, 1]:.3f}",
+                  flush=True)
+            for lo in range(0, cus, cus // 8):
+                print(f"  blocks {lo:3d}-{lo + cus // 8 - 1:3d}: start {sa[lo:lo + cus // 8].mean():5.2f} us, "
+                      f"end {ea[lo:lo + cus // 8].mean():6.1f} us", flush=True)
+            for x in range(8):
+                sel = idx % 8 == x
+                print(f"  blockIdx % 8 == {x}: start {sa[sel].mean():5.2f} us, end {ea[sel].mean():6.1f} us", flush=True)
         med = [statistics.median(r[:, i]) for i in range(r.shape[1])]
         print(f"{name}: prologue (start -> past the last barrier) median {med[0]:.2f} us, slowest {med[1]:.2f} us; "
               f"start spread {med[2]:.2f} us; first start -> last end {med[3]:.1f} us; last end - median end "
