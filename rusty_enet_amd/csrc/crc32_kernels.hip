@@ -1314,6 +1314,12 @@ __global__ __launch_bounds__(kBlock) void crc32_wave_regs_kernel(UniformBatch u,
 // 16 partial ones (tools/dma_probe PROBE_SPLIT: 217-219 us vs 224-229 us for the piece
 // loads, same box, alternating).
 // ---------------------------------------------------------------------------------
+// The whole-line kernel's LDS: the ragged kernel's table layout (the replicated main block and the
+// unreplicated tree sets that tree_levels_asm reads), 76 KiB instead of the register kernels' 132.
+struct UniformLinesLds {
+  uint32_t tables[kLdsDwords];
+  uint32_t next_dispatch;
+};
 struct UniformRegsLds {
   uint32_t tables[kRegsLdsDwords];
   uint32_t next_dispatch;
@@ -1461,7 +1467,7 @@ typedef __attribute__((address_space(1))) const u32x4 GlobalU32x4;
 template <int NSL>
 __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatch u, uint32_t* __restrict__ out) {
   send_servers_home();
-  __shared__ __attribute__((aligned(16))) UniformRegsLds S;
+  __shared__ __attribute__((aligned(16))) UniformLinesLds S;
   uint32_t* const lds = S.tables;
   const LaneConsts c = lane_consts(u.base);
   const uint32_t lane = threadIdx.x & 63u;
@@ -1486,7 +1492,7 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
   // The table loads, then the first round's line loads (lane_base clamps a round past the
   // batch), then the table stores: the start pays one memory latency, not the table's and
   // then the first lines' in a row.
-  const RegsTableLoads tl = load_regs_tables();
+  const TableLoads<kTreeLevels> tl = load_tables<kTreeLevels>(kMainLevel, 0);
   issue_order_fence();
   {
     const uint64_t lb = lane_base(rnd0);
@@ -1496,11 +1502,12 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
       issue_order_fence();
     }
   }
-  store_regs_tables(lds, tl);
+  store_tables<kTreeLevels>(lds, kTreeDword, tl);
   __syncthreads();
   if (rnd0 >= rounds) return;
   uint32_t res = 0, j = 0;
   uint64_t res_round = 0;
+  uint32_t tree_a = 0x10000u;  // tree_levels_asm's address register (high half 1, kept)
   while (rnd0 < rounds) {
     uint32_t d = 0;
     if (lane == 0) d = atomicAdd(&S.next_dispatch, 1u);
@@ -1546,7 +1553,10 @@ __global__ __launch_bounds__(kBlock) void crc32_uniform_lines_kernel(UniformBatc
       h2 = ll.lo ? s2 : h2;
       h3 = ll.lo ? s3 : h3;
     }
-    const uint32_t y = combine_tree_rep(lds, h0, h1, h2, h3, c.lk);
+    uint32_t y = apply_rep(lds, h0, h1, c.lk.lp1, c.lk);  // in-lane Horner over the 4 word streams
+    y = apply_rep(lds, y, h2, c.lk.lp1, c.lk);
+    y = apply_rep(lds, y, h3, c.lk.lp1, c.lk);
+    y = tree_levels_asm(y, tree_a);
     const uint32_t reg = finish_word(lds, y, 0u, c.lk);
     const uint32_t crc = (uint32_t)__shfl((int)__builtin_bswap32(~reg), (int)(lane & ~7u), 64);
     if (c.k == j) {
