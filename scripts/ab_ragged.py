@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import time
 import json
 import os
 import sys
@@ -45,6 +46,8 @@ def main() -> int:
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--configs", default="g2,frag")
     ap.add_argument("--unchecked-b", action="store_true", help="B is a measurement build: do not compare its output")
+    ap.add_argument("--cold", type=float, default=0.0,
+                    help="idle this many seconds before each block (then 5 untimed launches): the cold window")
     args = ap.parse_args()
 
     import torch
@@ -109,6 +112,11 @@ def main() -> int:
         times = {"a": [], "b": []}
         for blk in range(args.blocks):
             for key, f, out in (("a", fa, oa), ("b", fb, ob)) if blk % 2 == 0 else (("b", fb, ob), ("a", fa, oa)):
+                if args.cold > 0:
+                    torch.cuda.synchronize()
+                    time.sleep(args.cold)
+                    for _ in range(4):
+                        run(f, out)
                 run(f, out)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
