@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """Randomized ragged batches through the product against the oracle (tooling, GPU box).
 
-    python scripts/fuzz_ragged.py [--batches 60] [--seconds 150]
+    python scripts/fuzz_ragged.py [--batches 60] [--seconds 150] [--uniform 0.25]
 
 Each batch draws a count (4096-300,000), a length distribution (uniform ranges, MTU-sized
 mixes, tiny packets, bimodal, 128-B step edges, with zero-length packets), gaps between
 packets, overlaps and a base offset 0-15, then checks every checksum against the C oracle
-(16 threads).  Stops at the first mismatch and prints the batch's parameters."""
+(16 threads).  A share of the batches (--uniform) goes through the uniform entry instead:
+back-to-back packets of one 16-B multiple length (the whole-line kernel, with the register
+kernel for the head and tail) or of any length and stride.  Stops at the first mismatch and
+prints the batch's parameters."""
 import argparse
 import os
 import sys
@@ -53,6 +56,7 @@ def main() -> int:
     ap.add_argument("--batches", type=int, default=60)
     ap.add_argument("--seconds", type=float, default=150.0)
     ap.add_argument("--seed", type=int, default=20261017)
+    ap.add_argument("--uniform", type=float, default=0.0, help="share of batches through the uniform entry")
     args = ap.parse_args()
     import torch
 
@@ -67,6 +71,28 @@ def main() -> int:
     for b in range(args.batches):
         if time.time() - t0 > args.seconds:
             break
+        if rng.random() < args.uniform:
+            n = int(rng.integers(4096, 300_001))
+            if rng.random() < 0.7:  # whole-line shapes: 16-B multiples 528..1792, back to back
+                length = int(rng.integers(33, 113)) * 16
+                stride, base = length, int(rng.integers(0, 9)) * 16
+            else:
+                length = int(rng.integers(0, 2100))
+                stride, base = length + int(rng.integers(0, 40)), int(rng.integers(0, 16))
+            total = (n - 1) * stride + length + base + 8
+            data = rng.integers(0, 256, size=total, dtype=np.uint8)
+            d = torch.from_numpy(data).to(dev)[base:]
+            got = rea.crc32_batch(d, stride=stride, length=length, count=n).cpu().numpy().view(np.uint32)
+            want = _oracle.crc32_uniform(data[base:], stride, length, n, threads=16)
+            bad = np.flatnonzero(got != want)
+            if bad.size:
+                print(f"MISMATCH batch {b}: uniform length {length} stride {stride} base +{base} n {n} bad {bad.size}; "
+                      f"first packet {int(bad[0])}", flush=True)
+                return 1
+            done += 1
+            packets += n
+            print(f"batch {b}: uniform length {length} stride {stride} base +{base} n {n} ok", flush=True)
+            continue
         kind, base, starts, lengths = draw(rng)
         total = int((starts + lengths.astype(np.uint64)).max()) + base + 8
         data = rng.integers(0, 256, size=total, dtype=np.uint8)
